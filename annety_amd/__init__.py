@@ -1,0 +1,35 @@
+"""annety_amd — MI355X-native engine for annety's checksum path (CRC-32 batches on gfx950).
+
+Public surface:
+  Crc32c                  mirror of annety::Crc32c (include/Crc32c.h:22-83)
+  crc32_batch             device-resident fixed-length batch   (C-ABI annety_crc32_batch_fixed)
+  crc32_batch_var         device-resident variable-length batch (annety_crc32_batch_var)
+  crc32_update_batch      raw-register batch update            (annety_crc32_update_batch_fixed)
+  crc32_batch_host        host-memory batch, staged over PCIe  (annety_crc32_batch_fixed_host)
+  crc32_combine           join two digests                     (annety_crc32_combine)
+  sharded                 multi-GPU batch sharding helpers (torch.distributed / RCCL)
+"""
+from .crc32c import (  # noqa: F401
+    Crc32c,
+    crc32_batch,
+    crc32_batch_host,
+    crc32_batch_var,
+    crc32_combine,
+    crc32_update_batch,
+    digests_to_numpy,
+    tables,
+)
+from ._lib import CrcError, lib_path  # noqa: F401
+
+__all__ = [
+    "Crc32c",
+    "crc32_batch",
+    "crc32_batch_var",
+    "crc32_update_batch",
+    "crc32_batch_host",
+    "crc32_combine",
+    "digests_to_numpy",
+    "tables",
+    "CrcError",
+    "lib_path",
+]

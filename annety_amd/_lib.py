@@ -1,0 +1,68 @@
+"""ctypes binding of libannety_crc.so — the same binding a maintainer would add to a Python caller of
+annety's checksum. Loading fails loudly: there is no CPU fallback for the batch
+path. The single-buffer functions are the reference's host scalar API and run on the CPU by design.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+from . import build as _build
+
+_c_size = ctypes.c_size_t
+_vp = ctypes.c_void_p
+_u32 = ctypes.c_uint32
+_u64 = ctypes.c_uint64
+
+# (name, restype, argtypes) — must match include/annety_crc.h exactly.
+SIGNATURES = [
+    ("annety_crc_abi_version", ctypes.c_int, []),
+    ("annety_crc_init", ctypes.c_int, [ctypes.c_int]),
+    ("annety_crc_shutdown", ctypes.c_int, []),
+    ("annety_crc_strerror", ctypes.c_char_p, [ctypes.c_int]),
+    ("annety_crc_last_hip_error", ctypes.c_int, []),
+    ("annety_crc32_long", _u32, [_vp, _c_size]),
+    ("annety_crc32_short", _u32, [_vp, _c_size]),
+    ("annety_crc32_update", None, [ctypes.POINTER(_u32), _vp, _c_size]),
+    ("annety_crc32_combine", _u32, [_u32, _u32, _u64]),
+    ("annety_crc32_table16", ctypes.POINTER(_u32), []),
+    ("annety_crc32_table256", ctypes.POINTER(_u32), []),
+    ("annety_crc32_batch_fixed", ctypes.c_int, [_vp, _c_size, _c_size, _c_size, _vp, _vp]),
+    ("annety_crc32_batch_var", ctypes.c_int, [_vp, _vp, _vp, _c_size, _vp, _vp]),
+    ("annety_crc32_update_batch_fixed", ctypes.c_int, [_vp, _vp, _c_size, _c_size, _c_size, _vp]),
+    ("annety_crc32_batch_fixed_host", ctypes.c_int, [_vp, _c_size, _c_size, _c_size, _vp]),
+]
+
+_lib: ctypes.CDLL | None = None
+
+
+class CrcError(RuntimeError):
+    def __init__(self, status: int, where: str):
+        lib = get()
+        msg = lib.annety_crc_strerror(status).decode()
+        hip = lib.annety_crc_last_hip_error()
+        super().__init__(f"{where}: {msg} (status {status}, hipError {hip})")
+        self.status = status
+
+
+def lib_path() -> str:
+    return _build.LIB
+
+
+def get() -> ctypes.CDLL:
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_build.LIB):
+            _build.build()  # raises if hipcc is unavailable: no silent fallback
+        lib = ctypes.CDLL(_build.LIB)
+        for name, res, args in SIGNATURES:
+            f = getattr(lib, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(status: int, where: str) -> None:
+    if status != 0:
+        raise CrcError(status, where)

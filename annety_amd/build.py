@@ -1,0 +1,69 @@
+"""Build the native engine in-tree: annety_amd/libannety_crc.so (HIP for gfx950 + the C-ABI shim).
+
+Used by __graft_entry__.build() and, on a GPU box whose snapshot lacks the .so, by the loader.
+Pure hipcc command lines (no torch extension machinery): the product is a plain C-ABI shared library.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+INCLUDE = os.path.join(ROOT, "include")
+LIB = os.path.join(PKG, "libannety_crc.so")
+SOURCES = ["crc32_kernels.hip", "crc32_capi.cpp"]
+HEADERS = ["crc32_kernels.h", "crc32_math.h"]
+ARCH = "gfx950"
+
+
+def hipcc() -> str:
+    for c in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if c and os.path.exists(c):
+            return c
+    raise FileNotFoundError("hipcc not found (ROCm toolchain required to build libannety_crc.so)")
+
+
+def _inputs() -> list[str]:
+    files = [os.path.join(CSRC, s) for s in SOURCES + HEADERS]
+    files.append(os.path.join(INCLUDE, "annety_crc.h"))
+    return files
+
+
+def up_to_date() -> bool:
+    if not os.path.exists(LIB):
+        return False
+    t = os.path.getmtime(LIB)
+    return all(os.path.getmtime(f) <= t for f in _inputs())
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and up_to_date():
+        return LIB
+    objs = []
+    tmp = os.path.join(PKG, "build")
+    os.makedirs(tmp, exist_ok=True)
+    common = ["-std=c++17", "-O3", "-fPIC", f"-I{INCLUDE}", f"-I{CSRC}", "-Wall"]
+    for s in SOURCES:
+        src = os.path.join(CSRC, s)
+        obj = os.path.join(tmp, s + ".o")
+        cmd = [hipcc()] + common + ["-c", src, "-o", obj]
+        if s.endswith(".hip"):
+            cmd[1:1] = [f"--offload-arch={ARCH}"]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+        objs.append(obj)
+    out_tmp = LIB + ".tmp"
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out_tmp] + objs
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    os.replace(out_tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force=True, verbose=True))

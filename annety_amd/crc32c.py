@@ -1,0 +1,172 @@
+"""Host-side mirror of annety's checksum API over the MI355X engine.
+
+`Crc32c` mirrors the reference class annety::Crc32c (include/Crc32c.h:22-83) method for method:
+same names, same argument meaning, same values. The single-buffer methods run on the calling CPU
+thread exactly like the reference's inline code (through the C-ABI's host functions); the batch
+functions below are the data-parallel hot path and run ONLY on the GPU — there is no CPU fallback.
+
+Batch functions take torch tensors resident on a ROCm device (torch is device-memory/stream plumbing
+here) or raw device pointers, and launch on the current torch stream unless one is given.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional, Union
+
+import numpy as np
+
+from . import _lib
+
+BytesLike = Union[bytes, bytearray, memoryview, np.ndarray]
+
+
+def _host_view(buff: BytesLike) -> tuple[int, int, object]:
+    """(address, length, keepalive) of a host byte buffer without copying when possible."""
+    if isinstance(buff, np.ndarray):
+        a = np.ascontiguousarray(buff).view(np.uint8).reshape(-1)
+        return a.ctypes.data, a.size, a
+    if isinstance(buff, str):
+        buff = buff.encode()
+    if isinstance(buff, (bytes, bytearray, memoryview)):
+        a = np.frombuffer(buff, dtype=np.uint8)
+        return (a.ctypes.data if a.size else 0), a.size, a
+    raise TypeError(f"expected a bytes-like object, got {type(buff).__name__}")
+
+
+class Crc32c:
+    """Drop-in mirror of annety::Crc32c (include/Crc32c.h:22-83)."""
+
+    @staticmethod
+    def crc32_short(buff: BytesLike, length: Optional[int] = None) -> int:
+        """include/Crc32c.h:41-55 (also the StringPiece overload :25-28)."""
+        addr, n, keep = _host_view(buff)
+        n = n if length is None else min(length, n)
+        return int(_lib.get().annety_crc32_short(addr, n))
+
+    @staticmethod
+    def crc32_long(buff: BytesLike, length: Optional[int] = None) -> int:
+        """include/Crc32c.h:58-69 (also the StringPiece overload :30-33)."""
+        addr, n, keep = _host_view(buff)
+        n = n if length is None else min(length, n)
+        return int(_lib.get().annety_crc32_long(addr, n))
+
+    @staticmethod
+    def crc32_update(crc: int, buff: BytesLike, length: Optional[int] = None) -> int:
+        """include/Crc32c.h:71-82. The reference updates `*crc` in place; Python returns the new
+        register (no init, no final xor)."""
+        addr, n, keep = _host_view(buff)
+        n = n if length is None else min(length, n)
+        s = ctypes.c_uint32(crc & 0xFFFFFFFF)
+        _lib.get().annety_crc32_update(ctypes.byref(s), addr, n)
+        return int(s.value)
+
+    # ---- additive batch API (device) ----
+    @staticmethod
+    def crc32_long_batch(data, n: int, length: int, stride: Optional[int] = None, out=None, stream=None):
+        return crc32_batch(data, n, length, stride, out, stream)
+
+    @staticmethod
+    def crc32_combine(crc_a: int, crc_b: int, len_b: int) -> int:
+        return crc32_combine(crc_a, crc_b, len_b)
+
+
+def crc32_combine(crc_a: int, crc_b: int, len_b: int) -> int:
+    """crc(A||B) from crc(A), crc(B) and |B|."""
+    return int(_lib.get().annety_crc32_combine(crc_a & 0xFFFFFFFF, crc_b & 0xFFFFFFFF, len_b))
+
+
+def tables() -> tuple[np.ndarray, np.ndarray]:
+    """The drop-in's annety::internal::crc32_table256/16 (src/Crc32c.cc:20-92)."""
+    lib = _lib.get()
+    t256 = np.ctypeslib.as_array(lib.annety_crc32_table256(), shape=(256,)).copy()
+    t16 = np.ctypeslib.as_array(lib.annety_crc32_table16(), shape=(16,)).copy()
+    return t256, t16
+
+
+# ---------------- device batch path ----------------
+def _dev_ptr(x) -> int:
+    if isinstance(x, int):
+        return x
+    return int(x.data_ptr())
+
+
+def _stream_handle(stream, like) -> int:
+    if stream is None:
+        import torch
+
+        dev = like.device if hasattr(like, "device") else None
+        return int(torch.cuda.current_stream(dev).cuda_stream)
+    if isinstance(stream, int):
+        return stream
+    return int(stream.cuda_stream)
+
+
+def _require_device(t, name: str) -> None:
+    if hasattr(t, "is_cuda") and not t.is_cuda:
+        raise ValueError(f"{name} must be a device (ROCm) tensor; the batch path has no CPU fallback")
+
+
+def crc32_batch(data, n: int, length: int, stride: Optional[int] = None, out=None, stream=None):
+    """Digests of n fixed-length payloads: payload i = data[i*stride : i*stride + length].
+
+    `data`: uint8 device tensor (or raw device pointer with `out` given). Returns `out`, an int32 tensor
+    of n digests (bit pattern = the uint32 CRC; `.view(torch.uint32)` or `& 0xFFFFFFFF` to read).
+    """
+    import torch
+
+    stride = length if stride is None else stride
+    _require_device(data, "data")
+    if hasattr(data, "numel") and n > 0 and (n - 1) * stride + length > data.numel() * data.element_size():
+        raise ValueError("batch extends past the end of `data`")
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=data.device)
+    _require_device(out, "out")
+    st = _lib.get().annety_crc32_batch_fixed(_dev_ptr(data), n, length, stride, _dev_ptr(out),
+                                             _stream_handle(stream, out))
+    _lib.check(st, "annety_crc32_batch_fixed")
+    return out
+
+
+def crc32_batch_var(data, offsets, lengths, out=None, stream=None):
+    """Digests of payload i = data[offsets[i] : offsets[i] + lengths[i]] (any alignment).
+    offsets: int64 device tensor, lengths: int32 device tensor."""
+    import torch
+
+    _require_device(data, "data")
+    n = int(offsets.numel())
+    if offsets.dtype != torch.int64 or lengths.dtype != torch.int32 or lengths.numel() != n:
+        raise ValueError("offsets must be int64[n] and lengths int32[n]")
+    if out is None:
+        out = torch.empty(n, dtype=torch.int32, device=data.device)
+    st = _lib.get().annety_crc32_batch_var(_dev_ptr(data), _dev_ptr(offsets), _dev_ptr(lengths), n, _dev_ptr(out),
+                                           _stream_handle(stream, out))
+    _lib.check(st, "annety_crc32_batch_var")
+    return out
+
+
+def crc32_update_batch(state, data, n: int, length: int, stride: Optional[int] = None, stream=None):
+    """In-place raw-register update (crc32_update semantics) of state[i] over payload i."""
+    stride = length if stride is None else stride
+    _require_device(data, "data")
+    _require_device(state, "state")
+    st = _lib.get().annety_crc32_update_batch_fixed(_dev_ptr(state), _dev_ptr(data), n, length, stride,
+                                                    _stream_handle(stream, state))
+    _lib.check(st, "annety_crc32_update_batch_fixed")
+    return state
+
+
+def crc32_batch_host(buf: BytesLike, n: int, length: int, stride: Optional[int] = None) -> np.ndarray:
+    """Host-memory batch: staged to the current device and back (synchronous). Returns uint32[n]."""
+    stride = length if stride is None else stride
+    addr, size, keep = _host_view(buf)
+    if n > 0 and (n - 1) * stride + length > size:
+        raise ValueError("batch extends past the end of `buf`")
+    out = np.zeros(n, dtype=np.uint32)
+    st = _lib.get().annety_crc32_batch_fixed_host(addr, n, length, stride, out.ctypes.data)
+    _lib.check(st, "annety_crc32_batch_fixed_host")
+    return out
+
+
+def digests_to_numpy(out) -> np.ndarray:
+    """int32 device tensor of digests -> uint32 numpy array."""
+    return out.detach().cpu().numpy().view(np.uint32)

@@ -1,0 +1,477 @@
+// C-ABI shim of the MI355X checksum engine: argument checks, per-device table images, launch
+// selection, the host-memory staging pipeline, and the host scalar replacements of annety::Crc32c.
+// Declared in include/annety_crc.h; every entry point is reentrant and returns a status, never aborts.
+#include "annety_crc.h"
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstring>
+#include <mutex>
+#include <vector>
+
+#include "crc32_kernels.h"
+#include "crc32_math.h"
+
+using namespace annety_crc;
+
+namespace {
+
+thread_local int t_last_hip = 0;
+
+int hip_fail(hipError_t e) {
+  t_last_hip = static_cast<int>(e);
+  return e == hipErrorOutOfMemory ? ANNETY_CRC_ENOMEM : ANNETY_CRC_EHIP;
+}
+
+#define HIP_TRY(expr)                          \
+  do {                                         \
+    hipError_t e_ = (expr);                    \
+    if (e_ != hipSuccess) return hip_fail(e_); \
+  } while (0)
+
+// ---------------- host-built LDS images ----------------
+constexpr int kGroups[] = {1, 2, 4, 8, 16, 32};
+constexpr int kNumGroups = 6;
+
+int group_index(uint32_t g) {
+  for (int i = 0; i < kNumGroups; i++)
+    if ((uint32_t)kGroups[i] == g) return i;
+  return -1;
+}
+
+struct HostImages {
+  std::vector<uint32_t> slice;   // 32768 words
+  std::vector<uint32_t> groups;  // kNumGroups * (kGroupImageBytes / 4)
+  std::vector<uint32_t> unshift; // 128 * 128 words
+  uint32_t short_init[4];
+};
+
+// Apply matrix m to (v << 4k) for every nibble value: the 16-entry table of one nibble position.
+void nibble_tables(const Gf2Mat& m, uint32_t* out /* [8][16] */) {
+  for (int kk = 0; kk < 8; kk++)
+    for (uint32_t v = 0; v < 16; v++) out[kk * 16 + v] = gf2_apply(m, v << (4 * kk));
+}
+
+Gf2Mat gf2_inverse(const Gf2Mat& m) {
+  // Gauss-Jordan over GF(2) on rows of the 32x32 matrix (row r = bit r of every column)
+  uint64_t rows[32];
+  for (int r = 0; r < 32; r++) {
+    uint32_t row = 0;
+    for (int c = 0; c < 32; c++) row |= ((m.col[c] >> r) & 1u) << c;
+    rows[r] = (uint64_t)row | ((uint64_t)1 << (32 + r));  // [A | I]
+  }
+  for (int c = 0; c < 32; c++) {
+    int piv = c;
+    while (piv < 32 && !((rows[piv] >> c) & 1)) piv++;
+    std::swap(rows[c], rows[piv]);
+    for (int r = 0; r < 32; r++)
+      if (r != c && ((rows[r] >> c) & 1)) rows[r] ^= rows[c];
+  }
+  Gf2Mat inv{};
+  for (int c = 0; c < 32; c++) {
+    uint32_t col = 0;
+    for (int r = 0; r < 32; r++) col |= (uint32_t)((rows[r] >> (32 + c)) & 1u) << r;
+    inv.col[c] = col;
+  }
+  return inv;
+}
+
+const HostImages& host_images() {
+  static HostImages img;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    img.slice.assign(kLdsSliceBytes / 4, 0);
+    uint32_t t[4][256];
+    for (int kk = 0; kk < 4; kk++)
+      for (uint32_t e = 0; e < 256; e++) t[kk][e] = slice_entry(kk, e);
+    for (int P = 0; P < 2; P++)
+      for (uint32_t e = 0; e < 256; e++)
+        for (uint32_t r = 0; r < 32; r++) {
+          const uint32_t w = (P * 65536 + e * 256 + r * 8) / 4;
+          img.slice[w] = t[3 - 2 * P][e];      // P0: T3, P1: T1
+          img.slice[w + 1] = t[2 - 2 * P][e];  // P0: T2, P1: T0
+        }
+    const uint32_t gw = kGroupImageBytes / 4;
+    img.groups.assign((size_t)kNumGroups * gw, 0);
+    for (int gi = 0; gi < kNumGroups; gi++) {
+      const uint32_t G = kGroups[gi];
+      uint32_t* g = img.groups.data() + (size_t)gi * gw;
+      uint32_t nt[8 * 16];
+      for (uint32_t jj = 0; jj < G; jj++) {
+        nibble_tables(shift_matrix((uint64_t)(G - 1 - jj) * kChunkBytes), nt);
+        for (uint32_t slot = 0; slot < 32; slot++) {
+          if ((slot & (G - 1)) != jj) continue;
+          for (int kk = 0; kk < 8; kk++)
+            for (int v = 0; v < 16; v++) g[(kk * 2048 + v * 128 + slot * 4) / 4] = nt[kk * 16 + v];
+        }
+      }
+      nibble_tables(shift_matrix((uint64_t)(G - 1) * kChunkBytes), nt);
+      std::memcpy(g + kLdsJoinBytes / 4, nt, sizeof nt);
+    }
+    img.unshift.assign(128 * 128, 0);
+    const Gf2Mat inv1 = gf2_inverse(shift_matrix(1));
+    Gf2Mat acc{};
+    for (int i = 0; i < 32; i++) acc.col[i] = 1u << i;
+    for (int over = 0; over < 128; over++) {
+      nibble_tables(acc, img.unshift.data() + over * 128);
+      acc = gf2_mul(inv1, acc);
+    }
+    for (int l = 0; l < 4; l++) img.short_init[l] = shift_bits(kInit, 8u * l);
+  });
+  return img;
+}
+
+// ---------------- per-device state ----------------
+struct Staging {
+  void* h_pinned[2] = {nullptr, nullptr};  // pinned host ring
+  void* d_buf[2] = {nullptr, nullptr};
+  uint32_t* d_out[2] = {nullptr, nullptr};
+  uint32_t* h_out[2] = {nullptr, nullptr};
+  hipStream_t stream[2] = {nullptr, nullptr};
+  hipEvent_t done[2] = {nullptr, nullptr};
+  size_t bytes = 0, outs = 0;
+};
+
+struct DeviceCtx {
+  std::atomic<bool> ready{false};
+  int cus = 0;
+  void* d_slice = nullptr;
+  void* d_groups = nullptr;
+  uint32_t* d_unshift = nullptr;
+  uint32_t* d_short = nullptr;
+  Staging stg;
+  std::mutex stg_mu;  // one host-staged batch at a time per device
+};
+
+constexpr int kMaxDev = 64;
+DeviceCtx g_dev[kMaxDev];
+std::mutex g_init_mu;
+
+int init_device_locked(int dev) {
+  DeviceCtx& c = g_dev[dev];
+  if (c.ready) return ANNETY_CRC_OK;
+  int ndev = 0;
+  HIP_TRY(hipGetDeviceCount(&ndev));
+  if (dev < 0 || dev >= ndev) return ANNETY_CRC_ENODEV;
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, dev));
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0) return ANNETY_CRC_ENODEV;  // built for gfx950 only
+  int prev = 0;
+  HIP_TRY(hipGetDevice(&prev));
+  HIP_TRY(hipSetDevice(dev));
+  const HostImages& img = host_images();
+  int rc = ANNETY_CRC_OK;
+  do {
+    hipError_t e;
+    if ((e = hipMalloc(&c.d_slice, img.slice.size() * 4)) != hipSuccess) { rc = hip_fail(e); break; }
+    if ((e = hipMalloc(&c.d_groups, img.groups.size() * 4)) != hipSuccess) { rc = hip_fail(e); break; }
+    if ((e = hipMalloc(&c.d_unshift, img.unshift.size() * 4)) != hipSuccess) { rc = hip_fail(e); break; }
+    if ((e = hipMalloc(&c.d_short, 16)) != hipSuccess) { rc = hip_fail(e); break; }
+    if ((e = hipMemcpy(c.d_slice, img.slice.data(), img.slice.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_fail(e); break; }
+    if ((e = hipMemcpy(c.d_groups, img.groups.data(), img.groups.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_fail(e); break; }
+    if ((e = hipMemcpy(c.d_unshift, img.unshift.data(), img.unshift.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_fail(e); break; }
+    if ((e = hipMemcpy(c.d_short, img.short_init, 16, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_fail(e); break; }
+    c.cus = prop.multiProcessorCount;
+    c.ready = true;
+  } while (0);
+  (void)hipSetDevice(prev);
+  return rc;
+}
+
+int current_ctx(DeviceCtx** out) {
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  if (dev < 0 || dev >= kMaxDev) return ANNETY_CRC_ENODEV;
+  DeviceCtx& c = g_dev[dev];
+  if (!c.ready) {
+    std::lock_guard<std::mutex> lk(g_init_mu);
+    int rc = init_device_locked(dev);
+    if (rc != ANNETY_CRC_OK) return rc;
+  }
+  *out = &c;
+  return ANNETY_CRC_OK;
+}
+
+const void* group_image(const DeviceCtx& c, uint32_t g) {
+  return static_cast<const char*>(c.d_groups) + (size_t)group_index(g) * kGroupImageBytes;
+}
+
+uint32_t pick_group(uint64_t lines, size_t n, int cus) {
+  // Largest power of two <= lines, capped at 32 lanes; one more doubling (fewer rounds, same number of
+  // virtual lines) when the batch is too small to fill the chip.
+  uint32_t g = 1;
+  while (g < 32 && (uint64_t)g * 2 <= lines) g *= 2;
+  const size_t lanes_chip = (size_t)cus * fixed_kernel_block();
+  if (g < 32 && (uint64_t)g < lines && n * (size_t)g * 2 <= lanes_chip) g *= 2;
+  return g;
+}
+
+int run_fixed(DeviceCtx& c, const void* d_base, size_t n, size_t len, size_t stride, uint32_t* d_out, bool raw,
+              hipStream_t stream) {
+  FixedLaunch a{};
+  a.base = d_base;
+  a.n = n;
+  a.stride = stride;
+  a.len_blocks = (uint32_t)(len / 16);
+  const uint64_t lines = (len + kChunkBytes - 1) / kChunkBytes;
+  a.group = pick_group(lines, n, c.cus);
+  a.rounds = (uint32_t)((lines + a.group - 1) / a.group);
+  a.vlead = a.rounds * a.group * 8 - a.len_blocks;
+  a.full = a.vlead == 0;
+  a.raw = raw;
+  a.img_slice = c.d_slice;
+  a.img_group = group_image(c, a.group);
+  if (raw) {
+    const Gf2Mat m = shift_matrix(len);
+    std::memcpy(a.raw_shift_cols.c, m.col, sizeof m.col);
+  }
+  a.out = d_out;
+  a.max_blocks = (size_t)c.cus;
+  HIP_TRY(launch_fixed(a, stream));
+  return ANNETY_CRC_OK;
+}
+
+int run_var(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_off, const uint32_t* d_len,
+            uint64_t fstride, uint32_t flen, uint32_t group, uint32_t* d_out, hipStream_t stream) {
+  VarLaunch a{};
+  a.base = d_base;
+  a.n = n;
+  a.off = d_off;
+  a.len = d_len;
+  a.fixed_stride = fstride;
+  a.fixed_len = flen;
+  a.order = nullptr;
+  a.group = group;
+  a.img_slice = c.d_slice;
+  a.img_group = group_image(c, group);
+  a.unshift = c.d_unshift;
+  a.short_init = c.d_short;
+  a.out = d_out;
+  a.max_blocks = (size_t)c.cus;
+  HIP_TRY(launch_var(a, stream));
+  return ANNETY_CRC_OK;
+}
+
+bool fixed_fast_ok(const void* d_base, size_t len, size_t stride) {
+  return ((uintptr_t)d_base % 16 == 0) && (stride % 16 == 0) && (len % 16 == 0) && len >= 16 &&
+         len / 16 <= 0xFFFFFFFFull;
+}
+
+}  // namespace
+
+// ---------------- host scalar replacements (drop-in for include/Crc32c.h) ----------------
+namespace annety {
+namespace internal {
+// src/Crc32c.cc:20-92 — same symbols, same contents, generated from the polynomial at compile time.
+#define ANNETY_T256(i) annety_crc::table256_entry(i)
+#define ANNETY_R4(b) ANNETY_T256(b), ANNETY_T256(b + 1), ANNETY_T256(b + 2), ANNETY_T256(b + 3)
+#define ANNETY_R16(b) ANNETY_R4(b), ANNETY_R4(b + 4), ANNETY_R4(b + 8), ANNETY_R4(b + 12)
+#define ANNETY_R64(b) ANNETY_R16(b), ANNETY_R16(b + 16), ANNETY_R16(b + 32), ANNETY_R16(b + 48)
+uint32_t crc32_table256[256] = {ANNETY_R64(0u), ANNETY_R64(64u), ANNETY_R64(128u), ANNETY_R64(192u)};
+#define ANNETY_T16(i) annety_crc::table256_entry(16u * (i))
+uint32_t crc32_table16[16] = {ANNETY_T16(0u),  ANNETY_T16(1u),  ANNETY_T16(2u),  ANNETY_T16(3u),
+                              ANNETY_T16(4u),  ANNETY_T16(5u),  ANNETY_T16(6u),  ANNETY_T16(7u),
+                              ANNETY_T16(8u),  ANNETY_T16(9u),  ANNETY_T16(10u), ANNETY_T16(11u),
+                              ANNETY_T16(12u), ANNETY_T16(13u), ANNETY_T16(14u), ANNETY_T16(15u)};
+}  // namespace internal
+}  // namespace annety
+
+extern "C" {
+
+int annety_crc_abi_version(void) { return ANNETY_CRC_ABI_VERSION; }
+
+int annety_crc_init(int device) {
+  if (device < 0 || device >= kMaxDev) return ANNETY_CRC_ENODEV;
+  std::lock_guard<std::mutex> lk(g_init_mu);
+  return init_device_locked(device);
+}
+
+int annety_crc_shutdown(void) {
+  std::lock_guard<std::mutex> lk(g_init_mu);
+  int prev = 0;
+  if (hipGetDevice(&prev) != hipSuccess) prev = 0;
+  for (int d = 0; d < kMaxDev; d++) {
+    DeviceCtx& c = g_dev[d];
+    if (!c.ready) continue;
+    (void)hipSetDevice(d);
+    std::lock_guard<std::mutex> sl(c.stg_mu);
+    (void)hipFree(c.d_slice);
+    (void)hipFree(c.d_groups);
+    (void)hipFree(c.d_unshift);
+    (void)hipFree(c.d_short);
+    for (int i = 0; i < 2; i++) {
+      if (c.stg.stream[i]) (void)hipStreamDestroy(c.stg.stream[i]);
+      if (c.stg.done[i]) (void)hipEventDestroy(c.stg.done[i]);
+      if (c.stg.h_pinned[i]) (void)hipHostFree(c.stg.h_pinned[i]);
+      if (c.stg.h_out[i]) (void)hipHostFree(c.stg.h_out[i]);
+      if (c.stg.d_buf[i]) (void)hipFree(c.stg.d_buf[i]);
+      if (c.stg.d_out[i]) (void)hipFree(c.stg.d_out[i]);
+    }
+    c.stg = Staging{};
+    c.d_slice = c.d_groups = nullptr;
+    c.d_unshift = c.d_short = nullptr;
+    c.ready = false;
+  }
+  (void)hipSetDevice(prev);
+  return ANNETY_CRC_OK;
+}
+
+const char* annety_crc_strerror(int status) {
+  switch (status) {
+    case ANNETY_CRC_OK: return "ok";
+    case ANNETY_CRC_EINVAL: return "invalid argument";
+    case ANNETY_CRC_EHIP: return "HIP runtime error";
+    case ANNETY_CRC_ENOMEM: return "out of memory";
+    case ANNETY_CRC_ENODEV: return "no usable gfx950 device";
+    case ANNETY_CRC_ERCCL: return "collective failure";
+    default: return "unknown status";
+  }
+}
+
+int annety_crc_last_hip_error(void) { return t_last_hip; }
+
+// include/Crc32c.h:58-69
+uint32_t annety_crc32_long(const char* buff, size_t len) {
+  const unsigned char* p = reinterpret_cast<const unsigned char*>(buff);
+  uint32_t crc = kInit;
+  while (len--) crc = annety::internal::crc32_table256[(crc ^ *p++) & 0xff] ^ (crc >> 8);
+  return crc ^ kXorOut;
+}
+
+// include/Crc32c.h:41-55
+uint32_t annety_crc32_short(const char* buff, size_t len) {
+  const unsigned char* p = reinterpret_cast<const unsigned char*>(buff);
+  uint32_t crc = kInit;
+  while (len--) {
+    const unsigned c = *p++;
+    crc = annety::internal::crc32_table16[(crc ^ (c & 0xf)) & 0xf] ^ (crc >> 4);
+    crc = annety::internal::crc32_table16[(crc ^ (c >> 4)) & 0xf] ^ (crc >> 4);
+  }
+  return crc ^ kXorOut;
+}
+
+// include/Crc32c.h:71-82
+void annety_crc32_update(uint32_t* crc, const char* buff, size_t len) {
+  if (!crc) return;
+  const unsigned char* p = reinterpret_cast<const unsigned char*>(buff);
+  uint32_t c = *crc;
+  while (len--) c = annety::internal::crc32_table256[(c ^ *p++) & 0xff] ^ (c >> 8);
+  *crc = c;
+}
+
+uint32_t annety_crc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) { return combine(crc_a, crc_b, len_b); }
+
+const uint32_t* annety_crc32_table16(void) { return annety::internal::crc32_table16; }
+const uint32_t* annety_crc32_table256(void) { return annety::internal::crc32_table256; }
+
+int annety_crc32_batch_fixed(const void* d_base, size_t n, size_t len, size_t stride, uint32_t* d_out,
+                             void* stream) {
+  if (n == 0) return ANNETY_CRC_OK;
+  if (!d_out || (!d_base && len > 0) || (n > 1 && stride < len)) return ANNETY_CRC_EINVAL;
+  if (len > 0xFFFFFFFFull) return ANNETY_CRC_EINVAL;
+  DeviceCtx* c = nullptr;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (len == 0) {
+    HIP_TRY(hipMemsetAsync(d_out, 0, n * sizeof(uint32_t), s));  // crc of the empty string is 0
+    return ANNETY_CRC_OK;
+  }
+  if (fixed_fast_ok(d_base, len, stride)) return run_fixed(*c, d_base, n, len, stride, d_out, false, s);
+  const uint64_t lines = (len + 255) / 128;
+  return run_var(*c, d_base, n, nullptr, nullptr, stride, (uint32_t)len, pick_group(lines, n, c->cus), d_out, s);
+}
+
+int annety_crc32_batch_var(const void* d_base, const uint64_t* d_off, const uint32_t* d_len, size_t n,
+                           uint32_t* d_out, void* stream) {
+  if (n == 0) return ANNETY_CRC_OK;
+  if (!d_base || !d_off || !d_len || !d_out) return ANNETY_CRC_EINVAL;
+  DeviceCtx* c = nullptr;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  return run_var(*c, d_base, n, d_off, d_len, 0, 0, 8, d_out, static_cast<hipStream_t>(stream));
+}
+
+int annety_crc32_update_batch_fixed(uint32_t* d_state, const void* d_base, size_t n, size_t len, size_t stride,
+                                    void* stream) {
+  if (n == 0 || len == 0) return ANNETY_CRC_OK;  // no bytes: register unchanged
+  if (!d_state || !d_base || (n > 1 && stride < len)) return ANNETY_CRC_EINVAL;
+  if (!fixed_fast_ok(d_base, len, stride)) return ANNETY_CRC_EINVAL;  // raw path needs the aligned layout
+  DeviceCtx* c = nullptr;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  return run_fixed(*c, d_base, n, len, stride, d_state, true, static_cast<hipStream_t>(stream));
+}
+
+int annety_crc32_batch_fixed_host(const void* h_base, size_t n, size_t len, size_t stride, uint32_t* h_out) {
+  if (n == 0) return ANNETY_CRC_OK;
+  if (!h_out || (!h_base && len > 0) || (n > 1 && stride < len)) return ANNETY_CRC_EINVAL;
+  if (len == 0) {
+    std::memset(h_out, 0, n * sizeof(uint32_t));
+    return ANNETY_CRC_OK;
+  }
+  DeviceCtx* c = nullptr;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(c->stg_mu);
+  Staging& st = c->stg;
+  // Chunk of payloads per pipeline stage: ~64 MiB of packed payload bytes.
+  const size_t plen = (len + 15) & ~(size_t)15;  // packed, 16-byte aligned stride on the device
+  size_t per = std::max<size_t>(1, (64u << 20) / plen);
+  per = std::min(per, n);
+  const size_t need = per * plen;
+  if (st.bytes < need || st.outs < per) {
+    for (int i = 0; i < 2; i++) {
+      if (st.h_pinned[i]) (void)hipHostFree(st.h_pinned[i]);
+      if (st.d_buf[i]) (void)hipFree(st.d_buf[i]);
+      if (st.d_out[i]) (void)hipFree(st.d_out[i]);
+      if (st.h_out[i]) (void)hipHostFree(st.h_out[i]);
+      st.h_pinned[i] = st.d_buf[i] = nullptr;
+      st.d_out[i] = st.h_out[i] = nullptr;
+      st.bytes = st.outs = 0;
+      HIP_TRY(hipHostMalloc(&st.h_pinned[i], need, hipHostMallocDefault));
+      HIP_TRY(hipMalloc(&st.d_buf[i], need));
+      HIP_TRY(hipMalloc(reinterpret_cast<void**>(&st.d_out[i]), per * 4));
+      HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&st.h_out[i]), per * 4, hipHostMallocDefault));
+      if (!st.stream[i]) HIP_TRY(hipStreamCreateWithFlags(&st.stream[i], hipStreamNonBlocking));
+      if (!st.done[i]) HIP_TRY(hipEventCreateWithFlags(&st.done[i], hipEventDisableTiming));
+    }
+    st.bytes = need;
+    st.outs = per;
+  }
+  const char* src = static_cast<const char*>(h_base);
+  size_t pending_lo[2] = {0, 0}, pending_n[2] = {0, 0};
+  int slot = 0;
+  for (size_t lo = 0; lo < n; lo += per, slot ^= 1) {
+    const size_t cnt = std::min(per, n - lo);
+    if (pending_n[slot]) {  // drain the previous use of this slot
+      HIP_TRY(hipEventSynchronize(st.done[slot]));
+      std::memcpy(h_out + pending_lo[slot], st.h_out[slot], pending_n[slot] * 4);
+      pending_n[slot] = 0;
+    }
+    // pack payloads into the pinned slot (the host side of a NetBuffer -> device hand-off)
+    char* dst = static_cast<char*>(st.h_pinned[slot]);
+    if (stride == plen) {
+      std::memcpy(dst, src + lo * stride, cnt * plen - (plen - len));
+    } else {
+      for (size_t i = 0; i < cnt; i++) std::memcpy(dst + i * plen, src + (lo + i) * stride, len);
+    }
+    HIP_TRY(hipMemcpyAsync(st.d_buf[slot], dst, cnt * plen, hipMemcpyHostToDevice, st.stream[slot]));
+    rc = annety_crc32_batch_fixed(st.d_buf[slot], cnt, len, plen, st.d_out[slot], st.stream[slot]);
+    if (rc) return rc;
+    HIP_TRY(hipMemcpyAsync(st.h_out[slot], st.d_out[slot], cnt * 4, hipMemcpyDeviceToHost, st.stream[slot]));
+    HIP_TRY(hipEventRecord(st.done[slot], st.stream[slot]));
+    pending_lo[slot] = lo;
+    pending_n[slot] = cnt;
+  }
+  for (int i = 0; i < 2; i++)
+    if (pending_n[i]) {
+      HIP_TRY(hipEventSynchronize(st.done[i]));
+      std::memcpy(h_out + pending_lo[i], st.h_out[i], pending_n[i] * 4);
+    }
+  return ANNETY_CRC_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,104 @@
+// Shared host/device arithmetic for annety's checksum (reflected CRC-32/ISO-HDLC, poly 0xEDB88320).
+//
+// Reference semantics (restated, not copied):
+//   include/Crc32c.h:58-69  crc32_long  : c = ~0; for each byte c = T[(c ^ b) & 0xff] ^ (c >> 8); return ~c
+//   include/Crc32c.h:41-55  crc32_short : same value via two 16-entry nibble steps per byte
+//   include/Crc32c.h:71-82  crc32_update: the raw register loop without init / final xor
+//   src/Crc32c.cc:20-92     the 16- and 256-entry tables (generated here from the polynomial)
+//
+// Everything on the batch path is linear algebra over GF(2) on the 32-bit raw register:
+//   raw(M, s)         = register after absorbing bytes M from state s
+//   raw(A||B, s)      = shift_|B|(raw(A, s)) ^ raw(B, 0)
+//   shift_n(s)        = register after absorbing n zero bytes = the linear map x^(8n) mod P
+// The GPU kernels split each payload into 128-byte chunks owned by different lanes and re-join the
+// per-lane registers with precomputed shift_n maps.
+#pragma once
+
+#include <stddef.h>
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#define ANNETY_HD __host__ __device__
+#else
+#define ANNETY_HD
+#endif
+
+namespace annety_crc {
+
+constexpr uint32_t kPoly = 0xEDB88320u;  // reflected IEEE 802.3 polynomial (src/Crc32c.cc:8-9, table256[1])
+constexpr uint32_t kInit = 0xFFFFFFFFu;  // include/Crc32c.h:62
+constexpr uint32_t kXorOut = 0xFFFFFFFFu;  // include/Crc32c.h:68
+
+// One zero bit through the reflected register.
+ANNETY_HD constexpr uint32_t step_bit(uint32_t c) { return (c >> 1) ^ (kPoly & (0u - (c & 1u))); }
+
+// Register after n zero BITS (bit-serial; used for table generation and small shifts only).
+ANNETY_HD constexpr uint32_t shift_bits(uint32_t c, uint64_t nbits) {
+  for (uint64_t i = 0; i < nbits; i++) c = step_bit(c);
+  return c;
+}
+
+// table256[i] (src/Crc32c.cc:27-92) and the slicing tables T_k[e] = register after byte e followed by
+// k more zero bytes, i.e. 8*(k+1) bit steps from e.
+ANNETY_HD constexpr uint32_t table256_entry(uint32_t e) { return shift_bits(e, 8); }
+ANNETY_HD constexpr uint32_t slice_entry(int k, uint32_t e) { return shift_bits(e, 8u * (unsigned)(k + 1)); }
+
+// ---- GF(2) 32x32 matrices (columns = image of each bit) for arbitrary byte shifts, host side ----
+struct Gf2Mat {
+  uint32_t col[32];
+};
+
+ANNETY_HD inline uint32_t gf2_apply(const Gf2Mat& m, uint32_t v) {
+  uint32_t r = 0;
+  for (int i = 0; v; i++, v >>= 1)
+    if (v & 1u) r ^= m.col[i];
+  return r;
+}
+
+ANNETY_HD inline Gf2Mat gf2_mul(const Gf2Mat& a, const Gf2Mat& b) {  // a after b
+  Gf2Mat r{};
+  for (int i = 0; i < 32; i++) r.col[i] = gf2_apply(a, b.col[i]);
+  return r;
+}
+
+// Matrix of shift by n zero bytes, by binary powering of the one-byte map. O(32*32*log n).
+inline Gf2Mat shift_matrix(uint64_t nbytes) {
+  Gf2Mat byte{}, acc{};
+  for (int i = 0; i < 32; i++) {
+    byte.col[i] = shift_bits(1u << i, 8);
+    acc.col[i] = 1u << i;
+  }
+  while (nbytes) {
+    if (nbytes & 1) acc = gf2_mul(byte, acc);
+    byte = gf2_mul(byte, byte);
+    nbytes >>= 1;
+  }
+  return acc;
+}
+
+inline uint32_t shift_bytes(uint32_t c, uint64_t nbytes) { return gf2_apply(shift_matrix(nbytes), c); }
+
+// crc(A||B) from the FINAL values crc(A), crc(B) and |B| (zlib's identity; the init/xorout terms cancel).
+inline uint32_t combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) { return shift_bytes(crc_a, len_b) ^ crc_b; }
+
+// ---- LDS image layout of the batch kernels (bytes); see DESIGN.md §2 ----
+// [0, 128 KiB)          slicing-by-4 tables as two paired slots, 32 replicas:
+//                         pair P, entry e, replica r at P*65536 + e*256 + r*8 = {lo, hi}
+//                         P=0: {T3[e], T2[e]}   P=1: {T1[e], T0[e]}
+//                       read with ds_read_b64: address = one v_perm_b32, 32 lanes hit 32 distinct
+//                       8-byte slots of the 64-bank row -> conflict-free.
+// [128 KiB, 144 KiB)    lane-position join tables for a lane-group of G lanes, 32 replicas:
+//                         (k nibble, v value, slot s) at 131072 + k*2048 + v*128 + s*4
+//                         = shift_{(G-1-j)*128}(v << 4k), j = s & (G-1)
+// [144 KiB, +512 B)     round-advance tables (uniform across lanes -> broadcast reads):
+//                         (k, v) at 147456 + k*64 + v*4 = shift_{(G-1)*128}(v << 4k)
+constexpr uint32_t kLdsSliceBytes = 131072;
+constexpr uint32_t kLdsJoinOff = 131072;
+constexpr uint32_t kLdsJoinBytes = 16384;
+constexpr uint32_t kLdsRoundOff = 147456;
+constexpr uint32_t kLdsRoundBytes = 512;
+constexpr uint32_t kLdsImageBytes = kLdsRoundOff + kLdsRoundBytes;  // 147968
+constexpr uint32_t kGroupImageBytes = kLdsJoinBytes + kLdsRoundBytes;  // per-G part
+constexpr uint32_t kChunkBytes = 128;  // one cache line per lane per round
+
+}  // namespace annety_crc

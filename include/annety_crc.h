@@ -1,0 +1,87 @@
+/*
+ * annety_crc.h — C-ABI of the MI355X batch checksum engine (libannety_crc.so).
+ *
+ * Drop-in boundary for annety's checksum path. The reference API is the header-only class
+ * annety::Crc32c (include/Crc32c.h:22-83) over the tables in src/Crc32c.cc:20-92; it has no FFI.
+ * This header is what a foreign-language binding (ctypes, cgo, JNI, N-API) binds: plain pointers
+ * and sizes, `void*` for the hipStream_t, no C++ or torch types. The C++ drop-in header
+ * include/annety/Crc32c.h is layered on top of it.
+ *
+ * Checksum = CRC-32/ISO-HDLC (reflected poly 0xEDB88320, init 0xFFFFFFFF, xorout 0xFFFFFFFF), the
+ * exact function annety names "Crc32c" (SURVEY.md §0.1). Check value: crc("123456789") = 0xCBF43926.
+ *
+ * Error model (the reference functions are total): every entry point that can fail
+ * returns an int status, 0 on success, a negative ANNETY_CRC_E* code otherwise, and never aborts.
+ * Thread safety: all entry points are reentrant; device state is initialised once per device.
+ */
+#ifndef ANNETY_CRC_H
+#define ANNETY_CRC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define ANNETY_CRC_ABI_VERSION 1
+
+enum {
+  ANNETY_CRC_OK = 0,
+  ANNETY_CRC_EINVAL = -1,  /* bad argument (null pointer with n > 0, misaligned, length out of range) */
+  ANNETY_CRC_EHIP = -2,    /* HIP runtime error (see annety_crc_last_hip_error) */
+  ANNETY_CRC_ENOMEM = -3,  /* device or pinned-host allocation failed */
+  ANNETY_CRC_ENODEV = -4,  /* no usable gfx950 device */
+  ANNETY_CRC_ERCCL = -5    /* collective failure (multi-GPU helpers) */
+};
+
+/* ---- library / device lifecycle ---- */
+int annety_crc_abi_version(void);
+/* Uploads the LDS table images to `device` (idempotent; called lazily by every device entry point
+ * for the current device). */
+int annety_crc_init(int device);
+/* Frees device images and staging buffers of every initialised device. */
+int annety_crc_shutdown(void);
+const char* annety_crc_strerror(int status);
+/* Last hipError_t seen by this thread (0 if none). */
+int annety_crc_last_hip_error(void);
+
+/* ---- host scalar API: exact replacements of the reference's inline methods ----
+ * annety_crc32_long   replaces Crc32c::crc32_long(const char*, size_t)   include/Crc32c.h:58-69
+ * annety_crc32_short  replaces Crc32c::crc32_short(const char*, size_t)  include/Crc32c.h:41-55
+ * annety_crc32_update replaces Crc32c::crc32_update(uint32_t*, ...)      include/Crc32c.h:71-82
+ * These run on the calling CPU thread: a single frame is far below the size at which a device
+ * round trip pays; batches go through the device entry points below. */
+uint32_t annety_crc32_long(const char* buff, size_t len);
+uint32_t annety_crc32_short(const char* buff, size_t len);
+void annety_crc32_update(uint32_t* crc, const char* buff, size_t len);
+/* crc(A||B) from crc(A), crc(B) and |B| (GF(2) shift; not in the reference, used to join partials). */
+uint32_t annety_crc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b);
+/* The reference's table globals annety::internal::crc32_table16/256 (src/Crc32c.cc:20-92), read-only. */
+const uint32_t* annety_crc32_table16(void);
+const uint32_t* annety_crc32_table256(void);
+
+/* ---- device-resident batches (pointers are device memory of the current device) ----
+ * Fixed length: payload i occupies [d_base + i*stride, d_base + i*stride + len); d_out[i] receives
+ * crc32_long(payload i). Fast path: d_base 16-byte aligned, stride % 16 == 0, len % 16 == 0; other
+ * shapes are accepted and routed to the general kernel. `stream` is a hipStream_t (NULL = default).
+ * Asynchronous with respect to the host: results are valid after the stream is synchronised. */
+int annety_crc32_batch_fixed(const void* d_base, size_t n, size_t len, size_t stride, uint32_t* d_out,
+                             void* stream);
+/* Variable length: payload i = [d_base + d_off[i], + d_len[i]) (any alignment). */
+int annety_crc32_batch_var(const void* d_base, const uint64_t* d_off, const uint32_t* d_len, size_t n,
+                           uint32_t* d_out, void* stream);
+/* Raw-register update (crc32_update semantics) for a fixed-length batch: d_state[i] is the register
+ * before payload i on input and after it on output (no init, no final xor). */
+int annety_crc32_update_batch_fixed(uint32_t* d_state, const void* d_base, size_t n, size_t len, size_t stride,
+                                    void* stream);
+
+/* ---- host-memory batch (payloads off a NetBuffer/socket): staged through pinned buffers, H2D ->
+ * kernel -> D2H, pipelined on two streams. Synchronous. ---- */
+int annety_crc32_batch_fixed_host(const void* h_base, size_t n, size_t len, size_t stride, uint32_t* h_out);
+
+#ifdef __cplusplus
+} /* extern "C" */
+#endif
+
+#endif /* ANNETY_CRC_H */

@@ -1,0 +1,168 @@
+/*
+ * TEST INFRASTRUCTURE ONLY — CPU oracle for annety's checksum path.
+ *
+ * This file is the parity checker for the MI355X engine. Only tests/, __graft_entry__.smoke()
+ * and bench.py's cpu_baseline leg may load it. The product (libannety_crc.so) never links it.
+ *
+ * It restates, in plain C, the algorithm of the reference's checksum path:
+ *   - tables          : src/Crc32c.cc:20-25 (crc32_table16), src/Crc32c.cc:27-92 (crc32_table256)
+ *                       generated here from the reflected IEEE polynomial 0xEDB88320 instead of copied;
+ *   - crc32_long      : include/Crc32c.h:58-69   (byte-wise, 256-entry table)
+ *   - crc32_short     : include/Crc32c.h:41-55   (two nibble steps per byte, 16-entry table)
+ *   - crc32_update    : include/Crc32c.h:71-82   (raw register, no init / no final xor)
+ * plus batch drivers and helpers used by the tests (combine, LCG payload generator of SURVEY.md §8c).
+ *
+ * Parity is pinned: tests/test_oracle.py checks every function here against the compiled reference
+ * (oracle/_ref, built by oracle/Makefile from /root/reference/src/Crc32c.cc) through the golden
+ * fixtures in tests/golden/, and against Python's zlib.crc32.
+ */
+#include <stddef.h>
+#include <stdint.h>
+#include <string.h>
+#include <pthread.h>
+
+#define ORACLE_POLY 0xEDB88320u
+
+static uint32_t g_t256[256];
+static uint32_t g_t16[16];
+static int g_ready = 0;
+
+/* src/Crc32c.cc:27-92: entry i = 8 reflected shift/xor rounds of i. */
+static void oracle_build(void) {
+  for (uint32_t i = 0; i < 256; i++) {
+    uint32_t c = i;
+    for (int k = 0; k < 8; k++) c = (c >> 1) ^ (ORACLE_POLY & (0u - (c & 1u)));
+    g_t256[i] = c;
+  }
+  /* src/Crc32c.cc:20-25: the 16-entry table equals table256[16*i]. */
+  for (uint32_t i = 0; i < 16; i++) g_t16[i] = g_t256[16 * i];
+  g_ready = 1;
+}
+
+static inline void ensure(void) {
+  if (!g_ready) oracle_build();
+}
+
+void oracle_tables(uint32_t* t256, uint32_t* t16) {
+  ensure();
+  memcpy(t256, g_t256, sizeof g_t256);
+  memcpy(t16, g_t16, sizeof g_t16);
+}
+
+/* include/Crc32c.h:58-69 */
+uint32_t oracle_crc32_long(const unsigned char* buf, size_t len) {
+  ensure();
+  uint32_t crc = 0xFFFFFFFFu;
+  while (len--) crc = g_t256[(crc ^ *buf++) & 0xff] ^ (crc >> 8);
+  return crc ^ 0xFFFFFFFFu;
+}
+
+/* include/Crc32c.h:41-55 (the reference uses `char c; c >> 4` — masked with & 0xf, so the
+ * signedness of char does not change the value). */
+uint32_t oracle_crc32_short(const unsigned char* buf, size_t len) {
+  ensure();
+  uint32_t crc = 0xFFFFFFFFu;
+  while (len--) {
+    unsigned c = *buf++;
+    crc = g_t16[(crc ^ (c & 0xf)) & 0xf] ^ (crc >> 4);
+    crc = g_t16[(crc ^ (c >> 4)) & 0xf] ^ (crc >> 4);
+  }
+  return crc ^ 0xFFFFFFFFu;
+}
+
+/* include/Crc32c.h:71-82 */
+void oracle_crc32_update(uint32_t* crc, const unsigned char* buf, size_t len) {
+  ensure();
+  uint32_t c = *crc;
+  while (len--) c = g_t256[(c ^ *buf++) & 0xff] ^ (c >> 8);
+  *crc = c;
+}
+
+/* Raw-register shift by n zero bytes (the linear map x^(8n) mod P). Used by combine. */
+static uint32_t gf2_times(const uint32_t* mat, uint32_t vec) {
+  uint32_t sum = 0;
+  for (int i = 0; vec; i++, vec >>= 1)
+    if (vec & 1) sum ^= mat[i];
+  return sum;
+}
+static void gf2_square(uint32_t* sq, const uint32_t* mat) {
+  for (int n = 0; n < 32; n++) sq[n] = gf2_times(mat, mat[n]);
+}
+uint32_t oracle_shift_bytes(uint32_t c, uint64_t nbytes) {
+  /* operator for one zero bit: column i = image of bit i */
+  uint32_t odd[32], even[32];
+  if (nbytes == 0 || c == 0) return c;
+  odd[0] = ORACLE_POLY;
+  for (int i = 1; i < 32; i++) odd[i] = 1u << (i - 1);
+  gf2_square(even, odd); /* 2 bits */
+  gf2_square(odd, even); /* 4 bits */
+  /* odd = 4 bits; square once more gives one byte in even, then walk the bits of nbytes */
+  for (;;) {
+    gf2_square(even, odd); /* 8 bits, 32 bits, ... */
+    if (nbytes & 1) c = gf2_times(even, c);
+    nbytes >>= 1;
+    if (!nbytes) break;
+    gf2_square(odd, even);
+    if (nbytes & 1) c = gf2_times(odd, c);
+    nbytes >>= 1;
+    if (!nbytes) break;
+  }
+  return c;
+}
+
+/* crc(A||B) from crc(A), crc(B), |B|  (final, conditioned values; zlib's identity) */
+uint32_t oracle_crc32_combine(uint32_t crc1, uint32_t crc2, uint64_t len2) {
+  return oracle_shift_bytes(crc1, len2) ^ crc2;
+}
+
+/* Batch drivers: payload i at base + i*stride (fixed) or base + off[i] (variable). */
+void oracle_crc32_batch_fixed(const unsigned char* base, size_t n, size_t len, size_t stride, uint32_t* out) {
+  for (size_t i = 0; i < n; i++) out[i] = oracle_crc32_long(base + i * stride, len);
+}
+void oracle_crc32_batch_var(const unsigned char* base, const uint64_t* off, const uint32_t* len, size_t n,
+                            uint32_t* out) {
+  for (size_t i = 0; i < n; i++) out[i] = oracle_crc32_long(base + off[i], len[i]);
+}
+
+/* Payload-parallel batch over T host threads (one worker per core, mirroring annety's one loop per
+ * thread, src/EventLoopPool.cc:55-66). Used only for the cpu_baseline leg of bench.py. */
+typedef struct {
+  const unsigned char* base;
+  size_t lo, hi, len, stride;
+  uint32_t* out;
+} job_t;
+static void* worker(void* p) {
+  job_t* j = (job_t*)p;
+  for (size_t i = j->lo; i < j->hi; i++) j->out[i] = oracle_crc32_long(j->base + i * j->stride, j->len);
+  return NULL;
+}
+int oracle_crc32_batch_fixed_mt(const unsigned char* base, size_t n, size_t len, size_t stride, uint32_t* out,
+                                int threads) {
+  ensure();
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_t tid[256];
+  job_t jobs[256];
+  for (int t = 0; t < threads; t++) {
+    jobs[t].base = base;
+    jobs[t].lo = n * (size_t)t / threads;
+    jobs[t].hi = n * (size_t)(t + 1) / threads;
+    jobs[t].len = len;
+    jobs[t].stride = stride;
+    jobs[t].out = out;
+    if (pthread_create(&tid[t], NULL, worker, &jobs[t]) != 0) return -1;
+  }
+  for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
+  return 0;
+}
+
+/* SURVEY.md §8c seeded payload generator: s = s*6364136223846793005 + 1442695040888963407 (mod 2^64),
+ * byte = s >> 56, filled sequentially across payloads. Returns the final state so callers can continue. */
+uint64_t oracle_lcg_fill(unsigned char* buf, size_t nbytes, uint64_t seed) {
+  uint64_t s = seed;
+  for (size_t i = 0; i < nbytes; i++) {
+    s = s * 6364136223846793005ull + 1442695040888963407ull;
+    buf[i] = (unsigned char)(s >> 56);
+  }
+  return s;
+}

@@ -1,0 +1,136 @@
+"""C-ABI boundary checks that need no GPU: the library loads, exports exactly what
+include/annety_crc.h declares, the host scalar API and the drop-in tables match the reference
+fixtures, and the C++ drop-in header compiles (and, where the reference tree exists, compiles the
+reference's own LengthHeaderCodec unchanged against it)."""
+import ctypes
+import os
+import re
+import subprocess
+import zlib
+
+import numpy as np
+import pytest
+
+import annety_amd
+from annety_amd import _lib
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "annety_crc.h")
+
+
+def H(x: str) -> int:
+    return int(x, 16)
+
+
+def declared_symbols():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(annety_crc\w*)\s*\(", src)))
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _lib.get()
+    syms = declared_symbols()
+    assert len(syms) >= 14
+    for s in syms:
+        assert hasattr(lib, s), s
+    # the ctypes table in _lib covers the whole header (the binding INTEGRATION.md documents)
+    assert sorted(n for n, _, _ in _lib.SIGNATURES) == syms
+    out = subprocess.run(["nm", "-D", "--defined-only", _lib.lib_path()], capture_output=True, text=True).stdout
+    for s in syms:
+        assert re.search(rf"\bT {s}$", out, re.M), s
+    # the reference's table globals, same C++ symbols as src/Crc32c.cc
+    assert "_ZN6annety8internal14crc32_table256E" in out
+    assert "_ZN6annety8internal13crc32_table16E" in out
+
+
+def test_abi_version_and_errors():
+    lib = _lib.get()
+    assert lib.annety_crc_abi_version() == 1
+    assert lib.annety_crc_strerror(-1) == b"invalid argument"
+    # argument errors are reported before any device is touched
+    assert lib.annety_crc32_batch_fixed(None, 4, 16, 16, None, None) == -1
+    assert lib.annety_crc32_batch_fixed(None, 0, 16, 16, None, None) == 0  # empty batch is a no-op
+    assert lib.annety_crc32_batch_var(None, None, None, 3, None, None) == -1
+    assert lib.annety_crc32_batch_fixed_host(None, 2, 16, 8, None) == -1  # stride < len
+
+
+def test_host_scalar_api_matches_reference(golden):
+    k = golden("kat.json")
+    for kat in k["kats"]:
+        data = bytes.fromhex(kat["hex"])
+        assert annety_amd.Crc32c.crc32_long(data) == H(kat["crc32_long"])
+        assert annety_amd.Crc32c.crc32_short(data) == H(kat["crc32_short"])
+    assert annety_amd.Crc32c.crc32_update(0, b"123456789") == H(k["update"]["from_zero_123456789"])
+    t256, t16 = annety_amd.tables()
+    assert [int(x) for x in t256] == [H(x) for x in k["table256"]]
+    assert [int(x) for x in t16] == [H(x) for x in k["table16"]]
+
+
+def test_host_combine(golden):
+    for c in golden("combine.json")["cases"]:
+        assert annety_amd.crc32_combine(H(c["crcA"]), H(c["crcB"]), c["lenB"]) == H(c["crcAB"])
+
+
+def test_scalar_random_vs_zlib():
+    rng = np.random.default_rng(11)
+    for _ in range(200):
+        a = rng.integers(0, 256, int(rng.integers(0, 5000)), dtype=np.uint8).tobytes()
+        assert annety_amd.Crc32c.crc32_long(a) == zlib.crc32(a)
+        assert annety_amd.Crc32c.crc32_short(a) == zlib.crc32(a)
+
+
+def test_batch_path_refuses_host_tensors():
+    torch = pytest.importorskip("torch")
+    with pytest.raises(ValueError, match="no CPU fallback"):
+        annety_amd.crc32_batch(torch.zeros(64, dtype=torch.uint8), 4, 16)
+
+
+CPP_DROPIN = r"""
+#define ANNETY_CRC_NO_STRINGPIECE
+#include "annety/Crc32c.h"
+#include <cstdio>
+#include <cstring>
+int main() {
+  const char* s = "123456789";
+  uint32_t st = 0;
+  annety::Crc32c::crc32_update(&st, s, 9);
+  int ok = annety::Crc32c::crc32_long(s, 9) == 0xCBF43926u && annety::Crc32c::crc32_short(s, 9) == 0xCBF43926u &&
+           st == 0x2DFD2D88u && annety::internal::crc32_table256[1] == 0x77073096u &&
+           annety::Crc32c::crc32_combine(annety::Crc32c::crc32_long(s, 4), annety::Crc32c::crc32_long(s + 4, 5), 5) ==
+               0xCBF43926u;
+  std::printf("%s\n", ok ? "OK" : "BAD");
+  return ok ? 0 : 1;
+}
+"""
+
+
+def test_cpp_dropin_header_links_and_runs(tmp_path):
+    src = tmp_path / "t.cc"
+    src.write_text(CPP_DROPIN)
+    exe = tmp_path / "t"
+    libdir = os.path.dirname(_lib.lib_path())
+    subprocess.run(["g++", "-std=c++11", "-O2", "-Wall", "-Wextra", "-Werror", f"-I{ROOT}/include", str(src), "-o",
+                    str(exe), f"-L{libdir}", "-lannety_crc", f"-Wl,-rpath,{libdir}"], check=True)
+    r = subprocess.run([str(exe)], capture_output=True, text=True)
+    assert r.returncode == 0 and r.stdout.strip() == "OK", r.stdout + r.stderr
+
+
+CODEC_TU = r"""
+// The reference's own framing codec, unchanged, compiled against the drop-in Crc32c.h.
+#include "codec/LengthHeaderCodec.h"
+#ifndef ANNETY_AMD_CRC32C_H
+#error "the reference Crc32c.h was picked up instead of the drop-in"
+#endif
+int main() { return 0; }
+"""
+
+
+@pytest.mark.skipif(not os.path.isdir("/root/reference/include/codec"), reason="reference tree not present")
+def test_reference_codec_compiles_against_dropin(tmp_path):
+    # include/annety/ first on the path so "Crc32c.h" resolves to the drop-in, the rest to the reference.
+    src = tmp_path / "codec.cc"
+    src.write_text(CODEC_TU)
+    r = subprocess.run(["g++", "-std=c++11", "-fsyntax-only", f"-I{ROOT}/include/annety", f"-I{ROOT}/include",
+                        "-I/root/reference/include", "-I/root/reference/src", str(src)], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-3000:]
