@@ -218,6 +218,64 @@ __global__ __launch_bounds__(kBlock) void crc32_fixed_kernel(const uint8_t* __re
   }
 }
 
+// Single-round fast path (payload = exactly G lines, 16-byte aligned; BASELINE config 1 is G = 8):
+// each step is one whole payload per lane-group, so there is no round state, and the per-lane line
+// pointer advances by a constant per task. Loads run one task ahead (A/B double buffer).
+template <int G>
+__global__ __launch_bounds__(kBlock) void crc32_oneround_kernel(const uint8_t* __restrict__ base, size_t n,
+                                                                size_t stride, const uint4* __restrict__ img_slice,
+                                                                const uint4* __restrict__ img_group,
+                                                                uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsImageBytes / 16];
+  const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
+
+  const uint32_t j = threadIdx.x & (G - 1);
+  const size_t gid = (blockIdx.x * (size_t)kBlock + threadIdx.x) / G;
+  const size_t ngroups = ((size_t)gridDim.x * kBlock) / G;
+  const int ntasks = gid < n ? (int)((n - 1 - gid) / ngroups + 1) : 0;
+  const size_t pstep = ngroups * stride;  // bytes between this group's consecutive payloads
+
+  LaneCtx k;
+  k.L0 = (threadIdx.x & 31) << 3;
+  k.L1 = k.L0 | (1u << 16);
+  k.slot4 = (threadIdx.x & 31) << 2;
+  const uint32_t sinit = j == 0 ? kInit : 0u;  // init == complement of the payload's first word
+
+  const uint8_t* lp = base + gid * stride + (size_t)j * kChunkBytes;
+  uint32_t* op = out + gid;
+  uint4 A[8], B[8];
+  if (ntasks > 0) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) A[i] = reinterpret_cast<const uint4*>(lp)[i];
+  }
+  load_image(lds4, img_slice, img_group);
+  __syncthreads();
+
+  auto finish = [&](uint32_t s) {
+    uint32_t t = s;
+    if constexpr (G > 1) t = group_xor_reduce<G>(nibble_map_lane(s, lds, k.slot4));
+    if (j == G - 1) *op = ~t;
+    op += ngroups;
+  };
+  for (int t = 0; t < ntasks; t += 2) {
+    if (t + 1 < ntasks) {
+      const uint4* s = reinterpret_cast<const uint4*>(lp + pstep);
+#pragma unroll
+      for (int i = 0; i < 8; i++) B[i] = s[i];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    finish(absorb_line(sinit, A, k));
+    if (t + 2 < ntasks) {
+      const uint4* s = reinterpret_cast<const uint4*>(lp + 2 * pstep);
+#pragma unroll
+      for (int i = 0; i < 8; i++) A[i] = s[i];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 1 < ntasks) finish(absorb_line(sinit, B, k));
+    lp += 2 * pstep;
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // General kernel: any alignment, any length (variable-length batches and odd fixed shapes).
 // Lines are the 128-byte lines of ABSOLUTE device memory, so every load is aligned and never leaves
@@ -351,6 +409,30 @@ hipError_t launch_g(const FixedLaunch& a, hipStream_t stream) {
   return hipGetLastError();
 }
 
+template <int G>
+hipError_t launch_one_g(const FixedLaunch& a, hipStream_t stream) {
+  const size_t lanes = a.n * (size_t)G;
+  size_t blocks = (lanes + kBlock - 1) / kBlock;
+  if (blocks > a.max_blocks) blocks = a.max_blocks;
+  if (blocks == 0) return hipSuccess;
+  hipLaunchKernelGGL((crc32_oneround_kernel<G>), dim3((unsigned)blocks), dim3(kBlock), 0, stream,
+                     static_cast<const uint8_t*>(a.base), a.n, a.stride, static_cast<const uint4*>(a.img_slice),
+                     static_cast<const uint4*>(a.img_group), a.out);
+  return hipGetLastError();
+}
+
+hipError_t launch_one(const FixedLaunch& a, hipStream_t stream) {
+  switch (a.group) {
+    case 1: return launch_one_g<1>(a, stream);
+    case 2: return launch_one_g<2>(a, stream);
+    case 4: return launch_one_g<4>(a, stream);
+    case 8: return launch_one_g<8>(a, stream);
+    case 16: return launch_one_g<16>(a, stream);
+    case 32: return launch_one_g<32>(a, stream);
+    default: return hipErrorInvalidValue;
+  }
+}
+
 template <bool FULL, bool RAW>
 hipError_t launch_full(const FixedLaunch& a, hipStream_t stream) {
   switch (a.group) {
@@ -367,6 +449,7 @@ hipError_t launch_full(const FixedLaunch& a, hipStream_t stream) {
 }  // namespace
 
 hipError_t launch_fixed(const FixedLaunch& a, hipStream_t stream) {
+  if (!a.raw && a.full && a.rounds == 1) return launch_one(a, stream);
   if (a.raw) return a.full ? launch_full<true, true>(a, stream) : launch_full<false, true>(a, stream);
   return a.full ? launch_full<true, false>(a, stream) : launch_full<false, false>(a, stream);
 }

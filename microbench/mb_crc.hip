@@ -10,7 +10,9 @@
 #include <vector>
 #include <algorithm>
 #include <cstring>
+#include <string>
 #include <thread>
+#include "annety_crc.h"
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { \
   fprintf(stderr, "HIP %s at %s:%d\n", hipGetErrorString(e_), __FILE__, __LINE__); exit(1);} } while (0)
@@ -891,7 +893,9 @@ static double time_ms(F f, int reps = 15) {
   return ms[ms.size() / 2];
 }
 
+static int ab_main();
 int main(int argc, char** argv) {
+  if (argc > 1 && std::string(argv[1]) == "ab") return ab_main();
   make_tables();
   const size_t n = 1u << 20;  // payloads
   const size_t L = 1024;
@@ -1114,5 +1118,43 @@ int main(int argc, char** argv) {
   COMP(F_S4R, 1024, 1, 256)
   COMP(F_S4R, 1024, 2, 256)
   COMP(F_S4R, 512, 2, 256)
+  return 0;
+}
+
+// A/B: product library (C-ABI) vs the microbench stripe8n kernel on the same buffer, interleaved.
+static int ab_main() {
+  make_tables();
+  const size_t n = 1u << 20, L = 1024, bytes = n * L;
+  uint4* d;
+  uint32_t *out1, *out2;
+  CK(hipMalloc(&d, bytes));
+  CK(hipMalloc(&out1, n * 4));
+  CK(hipMalloc(&out2, n * 4));
+  hipLaunchKernelGGL(fill_kernel, dim3(4096), dim3(256), 0, 0, d, bytes / 16, 0x1234ull);
+  std::vector<uint32_t> hct(1024);
+  for (int jj = 0; jj < 8; jj++) for (int kk = 0; kk < 8; kk++) for (int vv = 0; vv < 16; vv++)
+    hct[(jj * 8 + kk) * 16 + vv] = shift_bytes((uint32_t)vv << (4 * kk), (7 - jj) * 128);
+  uint32_t* dct; CK(hipMalloc(&dct, 4096)); CK(hipMemcpy(dct, hct.data(), 4096, hipMemcpyHostToDevice));
+  CK(hipDeviceSynchronize());
+  auto prod = [&] { if (annety_crc32_batch_fixed(d, n, L, L, out1, nullptr) != 0) { fprintf(stderr, "prod fail\n"); exit(1);} };
+  auto mb = [&] { hipLaunchKernelGGL((k_stripe8n<512, 0>), dim3(256), dim3(512), 0, 0, d, n, out2, dct); };
+  for (int round = 0; round < 4; round++) {
+    double a = time_ms(prod, 10), b = time_ms(mb, 10);
+    printf("round %d  product %.4f ms (%.1f GB/s)   microbench %.4f ms (%.1f GB/s)\n", round, a, (bytes + 4.0 * n) / a / 1e6, b,
+           (bytes + 4.0 * n) / b / 1e6);
+  }
+  std::vector<uint32_t> h1(n), h2(n);
+  CK(hipMemcpy(h1.data(), out1, n * 4, hipMemcpyDeviceToHost));
+  CK(hipMemcpy(h2.data(), out2, n * 4, hipMemcpyDeviceToHost));
+  printf("outputs %s\n", h1 == h2 ? "identical" : "DIFFER");
+  // back-to-back launches (no events between)
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  for (int which = 0; which < 2; which++) {
+    CK(hipEventRecord(e0));
+    for (int r = 0; r < 50; r++) { if (which == 0) prod(); else mb(); }
+    CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+    float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+    printf("%s back-to-back x50: %.4f ms/launch (%.1f GB/s)\n", which == 0 ? "product" : "microbench", ms / 50, (bytes + 4.0 * n) / (ms / 50) / 1e6);
+  }
   return 0;
 }
