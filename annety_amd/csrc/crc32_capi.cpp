@@ -42,9 +42,9 @@ int group_index(uint32_t g) {
 }
 
 struct HostImages {
-  std::vector<uint32_t> slice;   // 32768 words
+  std::vector<uint32_t> slice;   // common part: slicing tables (32768 words) + half-line join (128 words)
   std::vector<uint32_t> groups;  // kNumGroups * (kGroupImageBytes / 4)
-  std::vector<uint32_t> unshift; // 128 * 128 words
+  std::vector<uint32_t> unshift; // 24 maps x 128 words (U_lo[0..15], U_hi[0..7])
   uint32_t short_init[4];
 };
 
@@ -82,7 +82,7 @@ const HostImages& host_images() {
   static HostImages img;
   static std::once_flag once;
   std::call_once(once, [] {
-    img.slice.assign(kLdsSliceBytes / 4, 0);
+    img.slice.assign(kLdsCommonBytes / 4, 0);
     uint32_t t[4][256];
     for (int kk = 0; kk < 4; kk++)
       for (uint32_t e = 0; e < 256; e++) t[kk][e] = slice_entry(kk, e);
@@ -93,6 +93,7 @@ const HostImages& host_images() {
           img.slice[w] = t[3 - 2 * P][e];      // P0: T3, P1: T1
           img.slice[w + 1] = t[2 - 2 * P][e];  // P0: T2, P1: T0
         }
+    nibble_tables(shift_matrix(64), img.slice.data() + kLdsHalfOff / 4);  // half-line join
     const uint32_t gw = kGroupImageBytes / 4;
     img.groups.assign((size_t)kNumGroups * gw, 0);
     for (int gi = 0; gi < kNumGroups; gi++) {
@@ -110,13 +111,20 @@ const HostImages& host_images() {
       nibble_tables(shift_matrix((uint64_t)(G - 1) * kChunkBytes), nt);
       std::memcpy(g + kLdsJoinBytes / 4, nt, sizeof nt);
     }
-    img.unshift.assign(128 * 128, 0);
+    img.unshift.assign(24 * 128, 0);
     const Gf2Mat inv1 = gf2_inverse(shift_matrix(1));
     Gf2Mat acc{};
     for (int i = 0; i < 32; i++) acc.col[i] = 1u << i;
-    for (int over = 0; over < 128; over++) {
-      nibble_tables(acc, img.unshift.data() + over * 128);
+    Gf2Mat inv16{};
+    for (int m = 0; m < 16; m++) {  // U_lo[m] = shift_{-m}
+      nibble_tables(acc, img.unshift.data() + m * 128);
       acc = gf2_mul(inv1, acc);
+    }
+    inv16 = acc;  // shift_{-16}
+    for (int i = 0; i < 32; i++) acc.col[i] = 1u << i;
+    for (int h = 0; h < 8; h++) {  // U_hi[h] = shift_{-16h}
+      nibble_tables(acc, img.unshift.data() + (16 + h) * 128);
+      acc = gf2_mul(inv16, acc);
     }
     for (int l = 0; l < 4; l++) img.short_init[l] = shift_bits(kInit, 8u * l);
   });
@@ -233,25 +241,46 @@ int run_fixed(DeviceCtx& c, const void* d_base, size_t n, size_t len, size_t str
   return ANNETY_CRC_OK;
 }
 
-int run_var(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_off, const uint32_t* d_len,
-            uint64_t fstride, uint32_t flen, uint32_t group, uint32_t* d_out, hipStream_t stream) {
+int run_var(DeviceCtx& c, const void* d_base, size_t n, uint64_t fstride, uint32_t flen, uint32_t group,
+            const void* desc, const uint32_t* range, uint32_t* d_out, hipStream_t stream) {
   VarLaunch a{};
   a.base = d_base;
   a.n = n;
-  a.off = d_off;
-  a.len = d_len;
   a.fixed_stride = fstride;
   a.fixed_len = flen;
-  a.order = nullptr;
+  a.desc = desc;
+  a.range = range;
   a.group = group;
   a.img_slice = c.d_slice;
   a.img_group = group_image(c, group);
-  a.unshift = c.d_unshift;
+  a.img_unshift = c.d_unshift;
   a.short_init = c.d_short;
   a.out = d_out;
   a.max_blocks = (size_t)c.cus;
   HIP_TRY(launch_var(a, stream));
   return ANNETY_CRC_OK;
+}
+
+// Variable batch: bucket by line count on the device (no host round trip), then one launch per
+// length class with its own lane-group width. Scratch comes from the stream-ordered allocator.
+int run_var_sorted(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_off, const uint32_t* d_len,
+                   uint32_t* d_out, hipStream_t stream) {
+  const size_t rows_words = (size_t)bucket_blocks(n) * bucket_count();
+  const size_t head = (rows_words + 8) * sizeof(uint32_t);  // rows + ranges (16-byte multiple)
+  char* scratch = nullptr;
+  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&scratch), head + 16 * n, stream));
+  uint32_t* rows = reinterpret_cast<uint32_t*>(scratch);
+  uint32_t* ranges = rows + rows_words;
+  void* desc = scratch + head;
+  int rc = ANNETY_CRC_OK;
+  hipError_t e = launch_bucket(d_base, n, d_off, d_len, rows, ranges, desc, d_out, stream);
+  if (e != hipSuccess) rc = hip_fail(e);
+  const uint32_t groups[3] = {32, 8, 2};
+  for (int k = 0; k < 3 && rc == ANNETY_CRC_OK; k++)
+    rc = run_var(c, d_base, n, 0, 0, groups[k], desc, ranges + 2 * k, d_out, stream);
+  e = hipFreeAsync(scratch, stream);
+  if (rc == ANNETY_CRC_OK && e != hipSuccess) rc = hip_fail(e);
+  return rc;
 }
 
 bool fixed_fast_ok(const void* d_base, size_t len, size_t stride) {
@@ -381,7 +410,7 @@ int annety_crc32_batch_fixed(const void* d_base, size_t n, size_t len, size_t st
   }
   if (fixed_fast_ok(d_base, len, stride)) return run_fixed(*c, d_base, n, len, stride, d_out, false, s);
   const uint64_t lines = (len + 255) / 128;
-  return run_var(*c, d_base, n, nullptr, nullptr, stride, (uint32_t)len, pick_group(lines, n, c->cus), d_out, s);
+  return run_var(*c, d_base, n, stride, (uint32_t)len, pick_group(lines, n, c->cus), nullptr, nullptr, d_out, s);
 }
 
 int annety_crc32_batch_var(const void* d_base, const uint64_t* d_off, const uint32_t* d_len, size_t n,
@@ -391,7 +420,8 @@ int annety_crc32_batch_var(const void* d_base, const uint64_t* d_off, const uint
   DeviceCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
-  return run_var(*c, d_base, n, d_off, d_len, 0, 0, 8, d_out, static_cast<hipStream_t>(stream));
+  if (n > 0xFFFFFFFFull) return ANNETY_CRC_EINVAL;  // order[] holds 32-bit payload indices
+  return run_var_sorted(*c, d_base, n, d_off, d_len, d_out, static_cast<hipStream_t>(stream));
 }
 
 int annety_crc32_update_batch_fixed(uint32_t* d_state, const void* d_base, size_t n, size_t len, size_t stride,

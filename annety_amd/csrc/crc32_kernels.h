@@ -33,21 +33,29 @@ hipError_t launch_fixed(const FixedLaunch& a, hipStream_t stream);
 struct VarLaunch {
   const void* base;          // device base pointer
   size_t n;                  // payload count
-  const uint64_t* off;       // device offsets (or null: off = i * fixed_stride)
-  const uint32_t* len;       // device lengths (or null: len = fixed_len)
-  uint64_t fixed_stride;
-  uint32_t fixed_len;
-  const uint32_t* order;     // optional device permutation of payload indices
+  uint64_t fixed_stride;     // direct mode (desc == null): payload i at base + i*fixed_stride,
+  uint32_t fixed_len;        //   fixed_len bytes
+  const void* desc;          // sorted mode: uint4 {addr lo, addr hi, len, index} per task (launch_bucket)
+  const uint32_t* range;     // sorted mode: device [begin, end) into desc for this class
   uint32_t group;            // lanes per payload
   const void* img_slice;
   const void* img_group;
-  const uint32_t* unshift;   // 128 x 8 x 16 nibble tables of shift_{-over}
+  const void* img_unshift;   // 12 KiB two-level inverse-shift tables (LDS image part 3)
   const uint32_t* short_init;  // shift_len(0xFFFFFFFF) for len = 0..3
   uint32_t* out;
   size_t max_blocks;
 };
 
 hipError_t launch_var(const VarLaunch& a, hipStream_t stream);
+
+// Counting sort of a variable batch by 128-byte line count (longest first): writes desc[] (16 B per
+// non-empty payload), ranges[6] = {begin,end} of the G=32 / G=8 / G=2 classes, and out[p] = 0 for
+// zero-length payloads. Scratch: rows = bucket_blocks(n) * bucket_count() words, ranges = 8 words,
+// desc = 16*n bytes.
+hipError_t launch_bucket(const void* base, size_t n, const uint64_t* d_off, const uint32_t* d_len, uint32_t* rows,
+                         uint32_t* ranges, void* desc, uint32_t* out, hipStream_t stream);
+unsigned bucket_blocks(size_t n);
+int bucket_count();
 int fixed_kernel_block();
 
 }  // namespace annety_crc

@@ -87,18 +87,28 @@ inline uint32_t combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) { return
 //                         P=0: {T3[e], T2[e]}   P=1: {T1[e], T0[e]}
 //                       read with ds_read_b64: address = one v_perm_b32, 32 lanes hit 32 distinct
 //                       8-byte slots of the 64-bank row -> conflict-free.
-// [128 KiB, 144 KiB)    lane-position join tables for a lane-group of G lanes, 32 replicas:
-//                         (k nibble, v value, slot s) at 131072 + k*2048 + v*128 + s*4
+// [128 KiB, +512 B)     half-line join: (k, v) = shift_64(v << 4k), uniform (broadcast reads). A line is
+//                       folded as two independent 64-byte chains (2x ILP) joined by this map.
+// [+512 B, +16 KiB)     lane-position join tables for a lane-group of G lanes, 32 replicas:
+//                         (k nibble, v value, slot s) at kLdsJoinOff + k*2048 + v*128 + s*4
 //                         = shift_{(G-1-j)*128}(v << 4k), j = s & (G-1)
-// [144 KiB, +512 B)     round-advance tables (uniform across lanes -> broadcast reads):
-//                         (k, v) at 147456 + k*64 + v*4 = shift_{(G-1)*128}(v << 4k)
+// [.., +512 B)          round-advance tables (uniform across lanes -> broadcast reads):
+//                         (k, v) at kLdsRoundOff + k*64 + v*4 = shift_{(G-1)*128}(v << 4k)
 constexpr uint32_t kLdsSliceBytes = 131072;
-constexpr uint32_t kLdsJoinOff = 131072;
+constexpr uint32_t kLdsHalfOff = 131072;
+constexpr uint32_t kLdsCommonBytes = kLdsHalfOff + 512;  // slicing + half-line join: same for every G
+constexpr uint32_t kLdsJoinOff = kLdsCommonBytes;        // 131584
 constexpr uint32_t kLdsJoinBytes = 16384;
-constexpr uint32_t kLdsRoundOff = 147456;
+constexpr uint32_t kLdsRoundOff = kLdsJoinOff + kLdsJoinBytes;  // 147968
 constexpr uint32_t kLdsRoundBytes = 512;
-constexpr uint32_t kLdsImageBytes = kLdsRoundOff + kLdsRoundBytes;  // 147968
+constexpr uint32_t kLdsImageBytes = kLdsRoundOff + kLdsRoundBytes;  // 148480
 constexpr uint32_t kGroupImageBytes = kLdsJoinBytes + kLdsRoundBytes;  // per-G part
+// Variable-length kernel only: two-level inverse-shift tables (8 x 16 nibble entries per map)
+//   [kLdsUnshiftOff, +8 KiB)  U_lo[m] = shift_{-m} bytes, m = 0..15
+//   [+8 KiB, +4 KiB)          U_hi[h] = shift_{-16h} bytes, h = 0..7 -> shift_{-over} = U_hi[over>>4] o U_lo[over&15]
+constexpr uint32_t kLdsUnshiftOff = kLdsImageBytes;
+constexpr uint32_t kLdsUnshiftBytes = 24 * 512;
+constexpr uint32_t kLdsVarImageBytes = kLdsUnshiftOff + kLdsUnshiftBytes;  // 160768 <= 163840
 constexpr uint32_t kChunkBytes = 128;  // one cache line per lane per round
 
 }  // namespace annety_crc
