@@ -7,6 +7,7 @@ Public surface:
   crc32_update_batch      raw-register batch update            (annety_crc32_update_batch_fixed)
   crc32_batch_host        host-memory batch, staged over PCIe  (annety_crc32_batch_fixed_host)
   crc32_combine           join two digests                     (annety_crc32_combine)
+  LengthHeaderCodec       batched frame verify/build for annety's LengthHeaderCodec wire format
   sharded                 multi-GPU batch sharding helpers (torch.distributed / RCCL)
 """
 from .crc32c import (  # noqa: F401
@@ -20,6 +21,7 @@ from .crc32c import (  # noqa: F401
     tables,
 )
 from ._lib import CrcError, lib_path  # noqa: F401
+from .codec import LengthHeaderCodec  # noqa: F401
 
 __all__ = [
     "Crc32c",
@@ -30,6 +32,7 @@ __all__ = [
     "crc32_combine",
     "digests_to_numpy",
     "tables",
+    "LengthHeaderCodec",
     "CrcError",
     "lib_path",
 ]

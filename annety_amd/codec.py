@@ -1,0 +1,171 @@
+"""Batched LengthHeaderCodec: frame verify (decode) and frame build (encode) for annety's wire format.
+
+Mirrors annety::LengthHeaderCodec (include/codec/LengthHeaderCodec.h:37-231) with the checksum
+enabled: same length types, same max_payload rule, same return codes. Where the reference handles one
+frame per call on an I/O thread, this class handles a whole receive stream (decode) or a whole batch
+of payloads (encode) per call, with every CRC computed on the GPU:
+
+  decode_batch  = Codec::recv's loop (include/codec/Codec.h:52-76) over a stream: the host walks the
+                  length headers (annety_lhc_parse: a sequential chain, a few ns per frame), the device
+                  checks every trailer in one batch (annety_lhc_verify_batch); the frames delivered are
+                  those before the first bad one, exactly the reference's sequence of decode() results.
+  encode_batch  = one encode() per payload appended to one NetBuffer (:146-201): host plan of the
+                  output offsets (annety_lhc_encode_plan), then one device pass writing header, payload
+                  copy and trailer of every frame (annety_lhc_encode_batch).
+
+There is no CPU fallback: the checksum work runs on the device or the call fails.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from .crc32c import BytesLike, _dev_ptr, _host_view, _require_device, _stream_handle
+
+DEFAULT_MAX_PAYLOAD = 64 * 1024 * 1024  # LengthHeaderCodec ctor default (:50)
+
+
+@dataclass
+class DecodeResult:
+    """What Codec::recv would have produced on this stream.
+
+    payload_off/payload_len: the frames decode() returned 1 for, in order (offsets into the stream).
+    consumed: bytes those frames took (the reference's has_read total).
+    rt: the decode() result that ended the loop: 0 (incomplete / stream exhausted) or -1 (invalid
+        length or checksum: the reference shuts the connection down).
+    ok: per-frame checksum verdicts of every complete frame the header walk found (device output).
+    """
+
+    payload_off: np.ndarray
+    payload_len: np.ndarray
+    consumed: int
+    rt: int
+    ok: np.ndarray
+
+
+@dataclass
+class EncodeResult:
+    """frames: uint8 device tensor holding every accepted frame back to back; frame_off[i] = start of
+    payload i's frame; rt[i] = the reference's encode() result for payload i (1, 0 empty, -1 too long)."""
+
+    frames: object
+    frame_off: np.ndarray
+    rt: np.ndarray
+
+
+def recv_result(length_type: int, off: np.ndarray, ln: np.ndarray, used: int, invalid: bool,
+                ok: np.ndarray) -> DecodeResult:
+    """Codec::recv's outcome from the header walk and the per-frame checksum verdicts: frames are
+    delivered in order until the first bad checksum (decode -1 at :128-132), else until the walk
+    stopped (incomplete: 0; invalid length: -1 at :102-106)."""
+    bad = np.flatnonzero(ok == 0)
+    if bad.size:
+        k = int(bad[0])
+        return DecodeResult(off[:k], ln[:k], int(off[k]) - length_type, -1, ok)
+    return DecodeResult(off, ln, used, -1 if invalid else 0, ok)
+
+
+class LengthHeaderCodec:
+    kLengthType8 = 1
+    kLengthType16 = 2
+    kLengthType32 = 4
+    kLengthType64 = 8
+
+    def __init__(self, length_type: int = kLengthType32, enable_checksum: bool = True,
+                 max_payload: int = DEFAULT_MAX_PAYLOAD):
+        # constructor checks of :48-61
+        if length_type not in (1, 2, 4, 8):
+            raise ValueError(f"length_type must be 1, 2, 4 or 8, got {length_type}")
+        if not enable_checksum:
+            raise ValueError("the batch codec is the checksum path; enable_checksum=False has no device work")
+        self.length_type = int(length_type)
+        self.max_payload = int(max_payload)
+
+    # ---------------- decode ----------------
+    def parse(self, stream: BytesLike, max_frames: int | None = None):
+        """Host header walk (annety_lhc_parse): (payload_off u64[k], payload_len u32[k], consumed,
+        stopped_on_invalid_length)."""
+        addr, size, keep = _host_view(stream)
+        cap = size // (self.length_type + 4) + 1 if max_frames is None else int(max_frames)
+        off = np.zeros(cap, dtype=np.uint64)
+        ln = np.zeros(cap, dtype=np.uint32)
+        k, used = ctypes.c_size_t(), ctypes.c_size_t()
+        st = _lib.get().annety_lhc_parse(addr or None, size, self.length_type, self.max_payload, off.ctypes.data,
+                                         ln.ctypes.data, cap, ctypes.byref(k), ctypes.byref(used))
+        if st < 0:
+            _lib.check(st, "annety_lhc_parse")
+        return off[: k.value], ln[: k.value], int(used.value), st == 1
+
+    def verify(self, d_stream, d_off, d_len, out_ok=None, out_digest=None, stream=None):
+        """Device checksum check of located frames: ok uint8[n] (1 = trailer matches)."""
+        import torch
+
+        _require_device(d_stream, "d_stream")
+        n = int(d_off.numel())
+        if out_ok is None:
+            out_ok = torch.empty(n, dtype=torch.uint8, device=d_stream.device)
+        st = _lib.get().annety_lhc_verify_batch(_dev_ptr(d_stream), _dev_ptr(d_off), _dev_ptr(d_len), n,
+                                                _dev_ptr(out_ok), _dev_ptr(out_digest) if out_digest is not None
+                                                else None, _stream_handle(stream, out_ok))
+        _lib.check(st, "annety_lhc_verify_batch")
+        return out_ok
+
+    def decode_batch(self, stream: BytesLike, d_stream=None, device=None) -> DecodeResult:
+        """Codec::recv over a whole stream. `stream` is the host copy the headers are read from;
+        `d_stream` the same bytes in device memory (uploaded here when not given)."""
+        import torch
+
+        off, ln, used, invalid = self.parse(stream)
+        if d_stream is None:
+            addr, size, keep = _host_view(stream)
+            h = np.asarray(keep, dtype=np.uint8).reshape(-1)
+            h = h if h.flags.writeable else h.copy()  # torch.from_numpy wants a writable array
+            d_stream = torch.from_numpy(h).to(device if device is not None else "cuda")
+        n = off.size
+        if n:
+            d_off = torch.from_numpy(off.view(np.int64)).to(d_stream.device)
+            d_len = torch.from_numpy(ln.view(np.int32)).to(d_stream.device)
+            ok = self.verify(d_stream, d_off, d_len).cpu().numpy()
+        else:
+            ok = np.zeros(0, dtype=np.uint8)
+        return recv_result(self.length_type, off, ln, used, invalid, ok)
+
+    # ---------------- encode ----------------
+    def plan(self, lengths: np.ndarray):
+        """annety_lhc_encode_plan: (frame_off u64[n], rt i8[n], total bytes)."""
+        ln = np.ascontiguousarray(lengths, dtype=np.uint32)
+        off = np.zeros(ln.size, dtype=np.uint64)
+        rt = np.zeros(ln.size, dtype=np.int8)
+        total = ctypes.c_uint64()
+        st = _lib.get().annety_lhc_encode_plan(ln.ctypes.data, ln.size, self.length_type, self.max_payload,
+                                               off.ctypes.data, rt.ctypes.data, ctypes.byref(total))
+        _lib.check(st, "annety_lhc_encode_plan")
+        return off, rt, int(total.value)
+
+    def encode_batch(self, d_src, src_off: np.ndarray, lengths: np.ndarray, stream=None) -> EncodeResult:
+        """Frames for payload i = d_src[src_off[i] : src_off[i] + lengths[i]] (host index arrays)."""
+        import torch
+
+        _require_device(d_src, "d_src")
+        src_off = np.ascontiguousarray(src_off, dtype=np.uint64)
+        lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+        if src_off.size != lengths.size:
+            raise ValueError("src_off and lengths differ in size")
+        if lengths.size and int((src_off + lengths.astype(np.uint64)).max()) > d_src.numel():
+            raise ValueError("a payload extends past the end of d_src")
+        frame_off, rt, total = self.plan(lengths)
+        dev = d_src.device
+        frames = torch.empty(total, dtype=torch.uint8, device=dev)
+        n = lengths.size
+        if n and total:
+            d_soff = torch.from_numpy(src_off.view(np.int64)).to(dev)
+            d_len = torch.from_numpy(lengths.view(np.int32)).to(dev)
+            d_foff = torch.from_numpy(frame_off.view(np.int64)).to(dev)
+            st = _lib.get().annety_lhc_encode_batch(_dev_ptr(d_src), _dev_ptr(d_soff), _dev_ptr(d_len), n,
+                                                    self.length_type, self.max_payload, _dev_ptr(frames),
+                                                    _dev_ptr(d_foff), _stream_handle(stream, frames))
+            _lib.check(st, "annety_lhc_encode_batch")
+        return EncodeResult(frames, frame_off, rt)

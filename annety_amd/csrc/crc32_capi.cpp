@@ -504,4 +504,109 @@ int annety_crc32_batch_fixed_host(const void* h_base, size_t n, size_t len, size
   return ANNETY_CRC_OK;
 }
 
+// ---- LengthHeaderCodec frames ----
+static bool lhc_type_ok(int t) { return t == 1 || t == 2 || t == 4 || t == 8; }
+
+// include/codec/LengthHeaderCodec.h:71-137 without the CRC: signed big-endian length (peek_int*),
+// min_payload = checksum_length = 4, max_payload check, completeness check.
+int annety_lhc_parse(const void* h_stream, size_t size, int length_type, int64_t max_payload, uint64_t* payload_off,
+                     uint32_t* payload_len, size_t max_frames, size_t* n_frames, size_t* consumed) {
+  if (!n_frames || !consumed || !lhc_type_ok(length_type) || (!h_stream && size) ||
+      (max_frames && (!payload_off || !payload_len)))
+    return ANNETY_CRC_EINVAL;
+  const unsigned char* p = static_cast<const unsigned char*>(h_stream);
+  const size_t T = (size_t)length_type;
+  size_t pos = 0, k = 0;
+  int rc = ANNETY_CRC_OK;
+  while (k < max_frames && size - pos >= T) {
+    uint64_t u = 0;
+    for (size_t b = 0; b < T; b++) u = (u << 8) | p[pos + b];
+    int64_t length;  // sign-extend like peek_int8/16/32/64
+    switch (T) {
+      case 1: length = (int8_t)u; break;
+      case 2: length = (int16_t)u; break;
+      case 4: length = (int32_t)u; break;
+      default: length = (int64_t)u; break;
+    }
+    if (length < 4 || (max_payload > 0 && length > max_payload)) {
+      rc = 1;  // decode returns -1: invalid length
+      break;
+    }
+    if (length - 4 > 0xFFFFFFFFll) {  // valid for the codec, but beyond this API's 32-bit lengths
+      rc = ANNETY_CRC_EINVAL;
+      break;
+    }
+    if (size - pos - T < (uint64_t)length) break;  // incomplete frame
+    payload_off[k] = pos + T;
+    payload_len[k] = (uint32_t)(length - 4);
+    k++;
+    pos += T + (size_t)length;
+  }
+  *n_frames = k;
+  *consumed = pos;
+  return rc;
+}
+
+int annety_lhc_verify_batch(const void* d_stream, const uint64_t* d_payload_off, const uint32_t* d_payload_len,
+                            size_t n, uint8_t* d_ok, uint32_t* d_digest, void* stream) {
+  if (n == 0) return ANNETY_CRC_OK;
+  if (!d_stream || !d_payload_off || !d_payload_len || !d_ok) return ANNETY_CRC_EINVAL;
+  DeviceCtx* c = nullptr;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  uint32_t* dig = d_digest;
+  if (!dig) HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&dig), n * sizeof(uint32_t), s));
+  rc = annety_crc32_batch_var(d_stream, d_payload_off, d_payload_len, n, dig, stream);
+  if (rc == ANNETY_CRC_OK) {
+    hipError_t e = launch_lhc_compare(d_stream, d_payload_off, d_payload_len, n, dig, d_ok, s);
+    if (e != hipSuccess) rc = hip_fail(e);
+  }
+  if (!d_digest) {
+    hipError_t e = hipFreeAsync(dig, s);
+    if (rc == ANNETY_CRC_OK && e != hipSuccess) rc = hip_fail(e);
+  }
+  return rc;
+}
+
+// LengthHeaderCodec::encode's per-payload decision (:169-176): rt 0 for an empty payload, -1 for
+// len > max_payload (max_payload > 0), else 1 with a frame of T + len + 4 bytes. Rejected payloads
+// get zero bytes, so the frames of the accepted ones are packed back to back as consecutive encode
+// calls on one NetBuffer would leave them.
+int annety_lhc_encode_plan(const uint32_t* h_len, size_t n, int length_type, int64_t max_payload,
+                           uint64_t* h_frame_off, int8_t* h_rt, uint64_t* total) {
+  if (!lhc_type_ok(length_type) || !total || (n && (!h_len || !h_frame_off))) return ANNETY_CRC_EINVAL;
+  uint64_t pos = 0;
+  for (size_t i = 0; i < n; i++) {
+    const uint32_t L = h_len[i];
+    const int8_t rt = L == 0 ? 0 : (max_payload > 0 && (int64_t)L > max_payload) ? -1 : 1;
+    if (h_rt) h_rt[i] = rt;
+    h_frame_off[i] = pos;
+    if (rt == 1) pos += (uint64_t)length_type + L + 4;
+  }
+  *total = pos;
+  return ANNETY_CRC_OK;
+}
+
+int annety_lhc_encode_batch(const void* d_src, const uint64_t* d_src_off, const uint32_t* d_len, size_t n,
+                            int length_type, int64_t max_payload, void* d_dst, const uint64_t* d_frame_off,
+                            void* stream) {
+  if (n == 0) return ANNETY_CRC_OK;
+  if (!lhc_type_ok(length_type) || !d_src || !d_src_off || !d_len || !d_dst || !d_frame_off) return ANNETY_CRC_EINVAL;
+  DeviceCtx* c = nullptr;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  uint32_t* dig = nullptr;
+  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&dig), n * sizeof(uint32_t), s));
+  rc = annety_crc32_batch_var(d_src, d_src_off, d_len, n, dig, stream);
+  if (rc == ANNETY_CRC_OK) {
+    hipError_t e = launch_lhc_encode(d_src, d_src_off, d_len, n, length_type, max_payload, d_dst, d_frame_off, dig, s);
+    if (e != hipSuccess) rc = hip_fail(e);
+  }
+  hipError_t e = hipFreeAsync(dig, s);
+  if (rc == ANNETY_CRC_OK && e != hipSuccess) rc = hip_fail(e);
+  return rc;
+}
+
 }  // extern "C"

@@ -56,6 +56,13 @@ hipError_t launch_bucket(const void* base, size_t n, const uint64_t* d_off, cons
                          uint32_t* ranges, void* desc, uint32_t* out, hipStream_t stream);
 unsigned bucket_blocks(size_t n);
 int bucket_count();
+
+// LengthHeaderCodec frames (crc32_frames.hip)
+hipError_t launch_lhc_compare(const void* stream_base, const uint64_t* off, const uint32_t* len, size_t n,
+                              const uint32_t* digest, uint8_t* ok, hipStream_t stream);
+hipError_t launch_lhc_encode(const void* src, const uint64_t* src_off, const uint32_t* len, size_t n, int T,
+                             int64_t max_payload, void* dst, const uint64_t* dst_off, const uint32_t* digest,
+                             hipStream_t stream);
 int fixed_kernel_block();
 
 }  // namespace annety_crc

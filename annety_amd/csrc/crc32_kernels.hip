@@ -129,7 +129,7 @@ __device__ __forceinline__ uint32_t group_xor_reduce(uint32_t x) {
 // straight into LDS with no VGPR round trip, so the whole image is in flight at once.
 // Parts: slicing tables (img_slice), the per-G join/round tables (img_group) and, for the
 // variable-length kernel, the inverse-shift tables (img_extra).
-template <uint32_t kBytes = kLdsImageBytes>
+template <uint32_t kBytes = kLdsImageBytes, int BLK = kBlock>
 __device__ __forceinline__ void load_image(uint4* lds4, const uint4* __restrict__ img_common,
                                            const uint4* __restrict__ img_group,
                                            const uint4* __restrict__ img_extra = nullptr) {
@@ -138,7 +138,7 @@ __device__ __forceinline__ void load_image(uint4* lds4, const uint4* __restrict_
   constexpr int kTotal = kBytes / 16;
   constexpr int kChunks = (kTotal + 63) / 64;  // 1 KiB pieces (the last one may be partial)
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int c = wave; c < kChunks; c += kBlock / 64) {
+  for (int c = wave; c < kChunks; c += BLK / 64) {
     const int i = c * 64 + lane;
     if (i < kTotal) {
       const uint4* src = i < kCommon ? img_common + i : (i < kBase ? img_group + (i - kCommon) : img_extra + (i - kBase));
@@ -259,8 +259,8 @@ __global__ __launch_bounds__(kBlock) void crc32_fixed_kernel(const uint8_t* __re
 // Single-round fast path (payload = exactly G lines, 16-byte aligned; BASELINE config 1 is G = 8):
 // each step is one whole payload per lane-group, so there is no round state, and the per-lane line
 // pointer advances by a constant per task. Loads run one task ahead (A/B double buffer).
-template <int G>
-__global__ __launch_bounds__(kBlock) void crc32_oneround_kernel(const uint8_t* __restrict__ base, size_t n,
+template <int G, int BLK = kBlock>
+__global__ __launch_bounds__(BLK) void crc32_oneround_kernel(const uint8_t* __restrict__ base, size_t n,
                                                                 size_t stride, const uint4* __restrict__ img_slice,
                                                                 const uint4* __restrict__ img_group,
                                                                 uint32_t* __restrict__ out) {
@@ -268,8 +268,8 @@ __global__ __launch_bounds__(kBlock) void crc32_oneround_kernel(const uint8_t* _
   const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
 
   const uint32_t j = threadIdx.x & (G - 1);
-  const size_t gid = (blockIdx.x * (size_t)kBlock + threadIdx.x) / G;
-  const size_t ngroups = ((size_t)gridDim.x * kBlock) / G;
+  const size_t gid = (blockIdx.x * (size_t)BLK + threadIdx.x) / G;
+  const size_t ngroups = ((size_t)gridDim.x * BLK) / G;
   const int ntasks = gid < n ? (int)((n - 1 - gid) / ngroups + 1) : 0;
   const size_t pstep = ngroups * stride;  // bytes between this group's consecutive payloads
 
@@ -286,7 +286,7 @@ __global__ __launch_bounds__(kBlock) void crc32_oneround_kernel(const uint8_t* _
 #pragma unroll
     for (int i = 0; i < 8; i++) A[i] = reinterpret_cast<const uint4*>(lp)[i];
   }
-  load_image(lds4, img_slice, img_group);
+  load_image<kLdsImageBytes, BLK>(lds4, img_slice, img_group);
   __syncthreads();
 
   auto finish = [&](uint32_t s) {

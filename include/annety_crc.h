@@ -80,6 +80,37 @@ int annety_crc32_update_batch_fixed(uint32_t* d_state, const void* d_base, size_
  * kernel -> D2H, pipelined on two streams. Synchronous. ---- */
 int annety_crc32_batch_fixed_host(const void* h_base, size_t n, size_t len, size_t stride, uint32_t* h_out);
 
+/* ---- LengthHeaderCodec wire format, batched ----
+ * frame = [length: T bytes big-endian, T = 1/2/4/8][payload: length-4 bytes][crc32(payload): 4 bytes BE]
+ * (include/codec/LengthHeaderCodec.h:33-46; decode :71-137; encode :146-201; checksum enabled). */
+
+/* Host walk of a receive stream, exactly LengthHeaderCodec::decode's framing without the CRC:
+ * from h_stream[0], for each complete frame writes its payload offset/length (relative to h_stream),
+ * stopping at the first incomplete frame, at max_frames, or at an invalid length (length < 4, or
+ * length > max_payload when max_payload > 0, or a negative signed length as peek_int* would read it).
+ * *n_frames = frames written, *consumed = bytes of those frames. Returns 0; 1 when it stopped on an
+ * invalid length at offset *consumed (decode's -1); ANNETY_CRC_EINVAL for a bad argument or a frame
+ * whose payload is 4 GiB or more (lengths here are 32-bit). */
+int annety_lhc_parse(const void* h_stream, size_t size, int length_type, int64_t max_payload, uint64_t* payload_off,
+                     uint32_t* payload_len, size_t max_frames, size_t* n_frames, size_t* consumed);
+/* Device verify of n frames already located (offsets/lengths from annety_lhc_parse, copied to the
+ * device): d_ok[i] = 1 if crc32_long(payload i) equals its big-endian trailer, else 0 (decode :123-132).
+ * d_digest (optional, may be NULL) receives the computed CRCs. */
+int annety_lhc_verify_batch(const void* d_stream, const uint64_t* d_payload_off, const uint32_t* d_payload_len,
+                            size_t n, uint8_t* d_ok, uint32_t* d_digest, void* stream);
+/* Host plan for a batch of LengthHeaderCodec::encode calls (:169-176): h_rt[i] (optional) = 1, or 0 for
+ * an empty payload, or -1 for len > max_payload (max_payload > 0); h_frame_off[i] = where frame i starts
+ * when the frames of accepted payloads are packed back to back (rejected ones take no bytes);
+ * *total = bytes of all frames. As in the reference, a length field too wide for T keeps its low T bytes. */
+int annety_lhc_encode_plan(const uint32_t* h_len, size_t n, int length_type, int64_t max_payload,
+                           uint64_t* h_frame_off, int8_t* h_rt, uint64_t* total);
+/* Device encode: for each accepted payload i = [d_src + d_src_off[i], + d_len[i]) writes header,
+ * payload copy and CRC trailer at d_dst + d_frame_off[i] (offsets from annety_lhc_encode_plan with the
+ * same length_type and max_payload); rejected payloads write nothing. */
+int annety_lhc_encode_batch(const void* d_src, const uint64_t* d_src_off, const uint32_t* d_len, size_t n,
+                            int length_type, int64_t max_payload, void* d_dst, const uint64_t* d_frame_off,
+                            void* stream);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

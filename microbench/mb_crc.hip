@@ -823,6 +823,13 @@ __global__ __launch_bounds__(BLK) void k_memvar(const uint4* __restrict__ d, siz
     step = ((size_t)gridDim.x * BLK) >> 3;
     first = gl;
     T = gl < n ? (int)((n - 1 - gl) / step + 1) : 0;
+  } else if (ASSIGN == 2) {
+    // virtual 256-thread workgroups: sub-block v of block b acts as block b + gridDim.x * v
+    const size_t vb = blockIdx.x + (size_t)gridDim.x * (threadIdx.x / 256);
+    const size_t gl = (vb * 256 + (threadIdx.x % 256)) >> 3;
+    step = ((size_t)gridDim.x * BLK) >> 3;
+    first = gl;
+    T = gl < n ? (int)((n - 1 - gl) / step + 1) : 0;
   } else {
     size_t per = (n + gridDim.x - 1) / gridDim.x;
     size_t b0 = blockIdx.x * per, b1 = b0 + per < n ? b0 + per : n;
@@ -896,6 +903,7 @@ static double time_ms(F f, int reps = 15) {
 static int ab_main();
 int main(int argc, char** argv) {
   if (argc > 1 && std::string(argv[1]) == "ab") return ab_main();
+  const bool mv_only = argc > 1 && std::string(argv[1]) == "mv";
   make_tables();
   const size_t n = 1u << 20;  // payloads
   const size_t L = 1024;
@@ -1090,10 +1098,10 @@ int main(int argc, char** argv) {
   }
 #define MV(BLK, AS, BUF, G) { double ms = time_ms([&] { hipLaunchKernelGGL((k_memvar<BLK, AS, BUF>), dim3(G), dim3(BLK), 0, 0, d, n, out); }); \
     printf("memvar blk=%d assign=%d buf=%d grid=%d  %.4f ms  %.1f GB/s\n", BLK, AS, BUF, G, ms, bytes / ms / 1e6); }
-  MV(512, 0, 1, 256) MV(512, 0, 2, 256) MV(512, 1, 1, 256) MV(512, 1, 2, 256)
-  MV(256, 0, 1, 256) MV(256, 0, 2, 256) MV(256, 1, 1, 256) MV(256, 1, 2, 256)
-  MV(256, 0, 1, 1024) MV(256, 0, 2, 1024) MV(256, 1, 1, 1024) MV(256, 1, 2, 1024)
-  MV(1024, 0, 1, 256) MV(1024, 0, 2, 256) MV(1024, 1, 1, 256) MV(1024, 1, 2, 256)
+  for (int rep = 0; rep < 2; rep++) {
+  MV(512, 0, 2, 256) MV(512, 2, 2, 256) MV(1024, 0, 2, 256) MV(1024, 2, 2, 256) MV(256, 0, 2, 1024) MV(256, 0, 2, 256) MV(768, 2, 2, 256)
+  }  if (mv_only) return 0;
+
   { double ms = time_ms([&] { hipLaunchKernelGGL(k_span<128>, dim3(256), dim3(512), 0, 0, d, bytes / 128, out); });
     printf("span128 blk512 grid256 %.4f ms %.1f GB/s\n", ms, bytes / ms / 1e6); }
 #define COMP(V, BLK, ILP, G)                                                                                 \

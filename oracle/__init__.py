@@ -22,6 +22,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB = os.path.join(HERE, "liboracle.so")
 _REF = os.path.join(HERE, "_ref", "libref_crc32.so")
+_REF_CODEC = os.path.join(HERE, "_ref", "libref_codec.so")
 
 _u8p = ctypes.POINTER(ctypes.c_uint8)
 _u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -61,6 +62,12 @@ def _load_oracle() -> ctypes.CDLL:
     lib.oracle_lcg_fill.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64]
     lib.oracle_tables.restype = None
     lib.oracle_tables.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    _sp = ctypes.POINTER(ctypes.c_size_t)
+    lib.oracle_lhc_encode.restype = ctypes.c_int
+    lib.oracle_lhc_encode.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t,
+                                      ctypes.c_void_p, _sp]
+    lib.oracle_lhc_decode.restype = ctypes.c_int
+    lib.oracle_lhc_decode.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t, _sp, _sp, _sp]
     return lib
 
 
@@ -148,6 +155,41 @@ def lcg_bytes(nbytes: int, seed: int) -> np.ndarray:
     return out
 
 
+# ---- LengthHeaderCodec frames (include/codec/LengthHeaderCodec.h), checksum enabled ----
+DEFAULT_MAX_PAYLOAD = 64 * 1024 * 1024  # LengthHeaderCodec ctor default (:50)
+
+
+def lhc_encode(payload, length_type: int = 4, max_payload: int = DEFAULT_MAX_PAYLOAD) -> tuple[int, bytes]:
+    """One LengthHeaderCodec::encode (:146-201): (rt, bytes appended to the stream)."""
+    a = _as_u8(payload)
+    out = np.zeros(a.size + 12, dtype=np.uint8)
+    n = ctypes.c_size_t()
+    rt = _lib.oracle_lhc_encode(length_type, max_payload, _ptr(a), a.size, _ptr(out), ctypes.byref(n))
+    return int(rt), out[: n.value].tobytes()
+
+
+def lhc_decode(stream, length_type: int = 4, max_payload: int = DEFAULT_MAX_PAYLOAD) -> tuple[int, int, int, int]:
+    """One LengthHeaderCodec::decode (:71-137): (rt, payload_off, payload_len, consumed)."""
+    a = _as_u8(stream)
+    off, ln, used = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+    rt = _lib.oracle_lhc_decode(length_type, max_payload, _ptr(a) if a.size else None, a.size, ctypes.byref(off),
+                                ctypes.byref(ln), ctypes.byref(used))
+    return int(rt), off.value, ln.value, used.value
+
+
+def lhc_recv(stream, length_type: int = 4, max_payload: int = DEFAULT_MAX_PAYLOAD):
+    """Codec::recv's loop (include/codec/Codec.h:52-76): decode while rt == 1.
+    Returns (frames [(payload_off, payload_len) relative to stream], consumed, last rt)."""
+    a = _as_u8(stream)
+    frames, pos = [], 0
+    while True:
+        rt, off, ln, used = lhc_decode(a[pos:], length_type, max_payload)
+        if rt != 1:
+            return frames, pos, rt
+        frames.append((pos + off, ln))
+        pos += used
+
+
 # ---- the compiled reference (only where /root/reference existed at build time) ----
 def ref_available() -> bool:
     return os.path.exists(_REF)
@@ -178,3 +220,16 @@ def ref_lib() -> ctypes.CDLL:
                                                  ctypes.c_void_p, ctypes.c_int]
         _ref = lib
     return _ref
+
+
+def ref_codec_lib() -> ctypes.CDLL:
+    """The reference's own LengthHeaderCodec (oracle/ref_codec.cc), for fixture generation."""
+    lib = ctypes.CDLL(_REF_CODEC)
+    _sp = ctypes.POINTER(ctypes.c_size_t)
+    lib.ref_lhc_encode.restype = ctypes.c_int
+    lib.ref_lhc_encode.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                   ctypes.c_size_t, _sp]
+    lib.ref_lhc_decode.restype = ctypes.c_int
+    lib.ref_lhc_decode.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                   ctypes.c_size_t, _sp, _sp]
+    return lib

@@ -166,3 +166,53 @@ uint64_t oracle_lcg_fill(unsigned char* buf, size_t nbytes, uint64_t seed) {
   }
   return s;
 }
+
+/* ---- LengthHeaderCodec frames (include/codec/LengthHeaderCodec.h), checksum enabled ----
+ * frame = [length: T bytes BE (signed, NetBuffer::peek_intN / append_intN, include/NetBuffer.h:38-125)]
+ *         [payload: length-4 bytes][crc32(payload): 4 bytes BE (append_int32 / peek_uint32 :18-23)] */
+
+/* append_intT(x) stores the low T bytes of x big-endian (the implicit narrowing to int8/16/32_t). */
+static void put_be(unsigned char* p, int T, uint64_t x) {
+  for (int b = 0; b < T; b++) p[b] = (unsigned char)(x >> (8 * (T - 1 - b)));
+}
+
+/* LengthHeaderCodec::encode (:146-201). Returns its rt (1 ok, 0 empty payload -> nothing written,
+ * -1 length > max_payload); *out_len = bytes appended. `out` must hold T + len + 4 bytes. */
+int oracle_lhc_encode(int T, int64_t max_payload, const unsigned char* payload, size_t len, unsigned char* out,
+                      size_t* out_len) {
+  *out_len = 0;
+  if (len == 0) return 0;                                   /* :169-171 */
+  if (max_payload > 0 && (int64_t)len > max_payload) return -1; /* :172-176 (min check is len < 0) */
+  put_be(out, T, (uint64_t)len + 4);                        /* :179 set_buff_length(length + 4) */
+  memcpy(out + T, payload, len);                            /* :180 */
+  put_be(out + T + len, 4, oracle_crc32_long(payload, len)); /* :185-196 long/short agree */
+  *out_len = (size_t)T + len + 4;
+  return 1;
+}
+
+/* One LengthHeaderCodec::decode call (:71-137) on `size` readable bytes. Returns its rt (1 frame,
+ * 0 incomplete, -1 invalid length or checksum); on 1, the payload is stream[*payload_off, +*payload_len)
+ * and *consumed = T + length bytes are removed. */
+int oracle_lhc_decode(int T, int64_t max_payload, const unsigned char* s, size_t size, size_t* payload_off,
+                      size_t* payload_len, size_t* consumed) {
+  *payload_off = *payload_len = *consumed = 0;
+  if (size < (size_t)T) return 0;                           /* :100 */
+  uint64_t u = 0;
+  for (int b = 0; b < T; b++) u = (u << 8) | s[b];
+  int64_t length;                                           /* :75-96 signed peek */
+  switch (T) {
+    case 1: length = (int8_t)u; break;
+    case 2: length = (int16_t)u; break;
+    case 4: length = (int32_t)u; break;
+    default: length = (int64_t)u; break;
+  }
+  if (length < 4 || (max_payload > 0 && length > max_payload)) return -1; /* :102-106, min_payload = 4 */
+  if (size - (size_t)T < (uint64_t)length) return 0;       /* :107 */
+  const unsigned char* tr = s + T + length - 4;            /* :112 */
+  uint32_t want = ((uint32_t)tr[0] << 24) | ((uint32_t)tr[1] << 16) | ((uint32_t)tr[2] << 8) | tr[3];
+  if (oracle_crc32_long(s + T, (size_t)length - 4) != want) return -1; /* :113-132 */
+  *payload_off = (size_t)T;
+  *payload_len = (size_t)length - 4;
+  *consumed = (size_t)T + (size_t)length;
+  return 1;
+}
