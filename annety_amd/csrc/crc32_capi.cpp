@@ -7,6 +7,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <vector>
@@ -151,6 +152,8 @@ struct DeviceCtx {
   uint32_t* d_short = nullptr;
   Staging stg;
   std::mutex stg_mu;  // one host-staged batch at a time per device
+  std::mutex pow_mu;  // split-path power tables, one per segment size
+  std::vector<std::pair<uint64_t, uint32_t*>> powers;
 };
 
 constexpr int kMaxDev = 64;
@@ -288,6 +291,94 @@ bool fixed_fast_ok(const void* d_base, size_t len, size_t stride) {
          len / 16 <= 0xFFFFFFFFull;
 }
 
+// ---- long payloads: end-aligned segments joined by the combine identity (see crc32_split_join) ----
+constexpr uint64_t kSegBytes = 65536;  // 512 lines: 16 rounds of a 32-lane group
+constexpr uint32_t kMaxSegs = 16384;
+
+// Tuning/test knobs, read per call: ANNETY_CRC_SPLIT=0 never splits, =1 splits whenever the payload
+// spans two segments, unset = auto; ANNETY_CRC_SEG overrides the minimum segment size (power of two).
+int split_mode() {
+  const char* e = std::getenv("ANNETY_CRC_SPLIT");
+  return e && *e ? std::atoi(e) : -1;
+}
+
+uint64_t split_min_segment() {
+  const char* e = std::getenv("ANNETY_CRC_SEG");
+  const unsigned long long v = e && *e ? std::strtoull(e, nullptr, 10) : 0;
+  return v >= 4096 && (v & (v - 1)) == 0 ? (uint64_t)v : kSegBytes;
+}
+
+// Segment size for a fixed-length batch, or 0 to run payloads whole.
+uint64_t split_segment(size_t n, uint64_t len, int cus) {
+  const int mode = split_mode();
+  if (mode == 0) return 0;
+  uint64_t seg = split_min_segment();
+  while ((len + seg - 1) / seg > kMaxSegs) seg *= 2;
+  if (len < 2 * seg) return 0;
+  const uint64_t S = (len + seg - 1) / seg;
+  if ((uint64_t)n * S > 0xFFFFFFFFull) return 0;  // descriptor indices are 32-bit
+  (void)cus;
+  // auto == 1: splitting measured faster on every long-payload shape tried, from 1 x 1 GiB to
+  // 4096 x 4 MiB, so a payload of two or more segments is always split.
+  return seg;
+}
+
+// powers[(m-1)*32 + b] = shift_{m*seg}(1 << b) for m = 1..kMaxSegs-1, built once per segment size.
+int split_powers(DeviceCtx& c, uint64_t seg, const uint32_t** out) {
+  std::lock_guard<std::mutex> lk(c.pow_mu);
+  for (auto& pw : c.powers)
+    if (pw.first == seg) {
+      *out = pw.second;
+      return ANNETY_CRC_OK;
+    }
+  std::vector<uint32_t> host((size_t)(kMaxSegs - 1) * 32);
+  const Gf2Mat step = shift_matrix(seg);
+  Gf2Mat cur = step;
+  for (uint32_t m = 1; m < kMaxSegs; m++) {
+    std::memcpy(&host[(size_t)(m - 1) * 32], cur.col, sizeof cur.col);
+    cur = gf2_mul(step, cur);
+  }
+  uint32_t* d = nullptr;
+  HIP_TRY(hipMalloc(reinterpret_cast<void**>(&d), host.size() * 4));
+  hipError_t e = hipMemcpy(d, host.data(), host.size() * 4, hipMemcpyHostToDevice);
+  if (e != hipSuccess) {
+    (void)hipFree(d);
+    return hip_fail(e);
+  }
+  c.powers.emplace_back(seg, d);
+  *out = d;
+  return ANNETY_CRC_OK;
+}
+
+int run_split(DeviceCtx& c, const void* d_base, size_t n, uint64_t len, uint64_t stride, uint64_t seg,
+              uint32_t* d_out, hipStream_t stream) {
+  const uint32_t S = (uint32_t)((len + seg - 1) / seg);
+  const size_t tasks = n * (size_t)S;
+  const uint32_t* powers = nullptr;
+  int rc = split_powers(c, seg, &powers);
+  if (rc) return rc;
+  const size_t crc_bytes = (tasks * 4 + 15) & ~(size_t)15;
+  char* scratch = nullptr;
+  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&scratch), 16 + crc_bytes + 16 * tasks, stream));
+  uint32_t* range = reinterpret_cast<uint32_t*>(scratch);
+  uint32_t* seg_crc = reinterpret_cast<uint32_t*>(scratch + 16);
+  void* desc = scratch + 16 + crc_bytes;
+  if (stride == len && len % seg == 0 && fixed_fast_ok(d_base, seg, seg)) {
+    // packed payloads whose length is a multiple of seg: the segments are one uniform fixed batch
+    rc = run_fixed(c, d_base, tasks, seg, seg, seg_crc, false, stream);
+  } else {
+    hipError_t e = launch_split_desc(d_base, n, len, stride, seg, S, desc, range, stream);
+    rc = e == hipSuccess ? run_var(c, d_base, tasks, 0, 0, 32, desc, range, seg_crc, stream) : hip_fail(e);
+  }
+  if (rc == ANNETY_CRC_OK) {
+    hipError_t e = launch_split_join(seg_crc, n, S, powers, d_out, stream);
+    if (e != hipSuccess) rc = hip_fail(e);
+  }
+  hipError_t e = hipFreeAsync(scratch, stream);
+  if (rc == ANNETY_CRC_OK && e != hipSuccess) rc = hip_fail(e);
+  return rc;
+}
+
 }  // namespace
 
 // ---------------- host scalar replacements (drop-in for include/Crc32c.h) ----------------
@@ -339,6 +430,11 @@ int annety_crc_shutdown(void) {
       if (c.stg.d_out[i]) (void)hipFree(c.stg.d_out[i]);
     }
     c.stg = Staging{};
+    {
+      std::lock_guard<std::mutex> pl(c.pow_mu);
+      for (auto& pw : c.powers) (void)hipFree(pw.second);
+      c.powers.clear();
+    }
     c.d_slice = c.d_groups = nullptr;
     c.d_unshift = c.d_short = nullptr;
     c.ready = false;
@@ -399,7 +495,6 @@ int annety_crc32_batch_fixed(const void* d_base, size_t n, size_t len, size_t st
                              void* stream) {
   if (n == 0) return ANNETY_CRC_OK;
   if (!d_out || (!d_base && len > 0) || (n > 1 && stride < len)) return ANNETY_CRC_EINVAL;
-  if (len > 0xFFFFFFFFull) return ANNETY_CRC_EINVAL;
   DeviceCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
@@ -408,6 +503,8 @@ int annety_crc32_batch_fixed(const void* d_base, size_t n, size_t len, size_t st
     HIP_TRY(hipMemsetAsync(d_out, 0, n * sizeof(uint32_t), s));  // crc of the empty string is 0
     return ANNETY_CRC_OK;
   }
+  if (const uint64_t seg = split_segment(n, len, c->cus)) return run_split(*c, d_base, n, len, stride, seg, d_out, s);
+  if (len > 0xFFFFFFFFull) return ANNETY_CRC_EINVAL;  // whole-payload kernels take 32-bit lengths
   if (fixed_fast_ok(d_base, len, stride)) return run_fixed(*c, d_base, n, len, stride, d_out, false, s);
   const uint64_t lines = (len + 255) / 128;
   return run_var(*c, d_base, n, stride, (uint32_t)len, pick_group(lines, n, c->cus), nullptr, nullptr, d_out, s);

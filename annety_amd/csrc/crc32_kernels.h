@@ -57,6 +57,13 @@ hipError_t launch_bucket(const void* base, size_t n, const uint64_t* d_off, cons
 unsigned bucket_blocks(size_t n);
 int bucket_count();
 
+// Long payloads cut into end-aligned segments (crc32_kernels.hip): descriptors for the variable kernel,
+// then the combine fold with powers[(m-1)*32 + bit] = shift_{m*seg}(1 << bit), m = 1..S-1.
+hipError_t launch_split_desc(const void* base, size_t n, uint64_t len, uint64_t stride, uint64_t seg, uint32_t S,
+                             void* desc, uint32_t* range, hipStream_t stream);
+hipError_t launch_split_join(const uint32_t* seg_crc, size_t n, uint32_t S, const uint32_t* powers, uint32_t* out,
+                             hipStream_t stream);
+
 // LengthHeaderCodec frames (crc32_frames.hip)
 hipError_t launch_lhc_compare(const void* stream_base, const uint64_t* off, const uint32_t* len, size_t n,
                               const uint32_t* digest, uint8_t* ok, hipStream_t stream);

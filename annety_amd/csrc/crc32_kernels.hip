@@ -21,6 +21,22 @@ namespace annety_crc {
 namespace {
 
 constexpr int kBlock = 512;
+// Threads per virtual workgroup (0 = off): the lane-groups of one 512-thread block are taken from
+// two virtual blocks gridDim.x apart instead of one contiguous run (microbench/mb_crc.hip `mv`:
+// 6.43 vs 6.17 TB/s for the same load/LDS structure).
+constexpr int kVwg = 256;
+
+// Lane-group index of this thread under the virtual-workgroup mapping (a bijection onto
+// [0, gridDim.x * BLK / G) for VWG a multiple of G that divides BLK).
+template <int BLK, int G, int VWG>
+__device__ __forceinline__ size_t group_id() {
+  if constexpr (VWG == 0 || VWG >= BLK) {
+    return (blockIdx.x * (size_t)BLK + threadIdx.x) / G;
+  } else {
+    const size_t v = blockIdx.x + (size_t)gridDim.x * (threadIdx.x / VWG);
+    return (v * VWG + threadIdx.x % VWG) / G;
+  }
+}
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
@@ -153,7 +169,7 @@ __device__ __forceinline__ void load_image(uint4* lds4, const uint4* __restrict_
 // lane's last chunk ends (G-1-j)*128 bytes before the payload end and the join maps are constants.
 //   FULL  : len is a multiple of G*128 (no virtual blocks)
 //   RAW   : crc32_update semantics - no init injection, no final xor; state_in folded in by the writer
-template <int G, bool FULL, bool RAW>
+template <int G, bool FULL, bool RAW, int VWG = kVwg>
 __global__ __launch_bounds__(kBlock) void crc32_fixed_kernel(const uint8_t* __restrict__ base, size_t n,
                                                              uint32_t len_blocks, size_t stride, uint32_t rounds,
                                                              uint32_t vlead, const uint4* __restrict__ img_slice,
@@ -164,7 +180,7 @@ __global__ __launch_bounds__(kBlock) void crc32_fixed_kernel(const uint8_t* __re
   const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
 
   const uint32_t j = threadIdx.x & (G - 1);
-  const size_t gid = (blockIdx.x * (size_t)kBlock + threadIdx.x) / G;
+  const size_t gid = group_id<kBlock, G, VWG>();
   const size_t ngroups = ((size_t)gridDim.x * kBlock) / G;
   const size_t ntasks = gid < n ? (n - 1 - gid) / ngroups + 1 : 0;
 
@@ -259,7 +275,7 @@ __global__ __launch_bounds__(kBlock) void crc32_fixed_kernel(const uint8_t* __re
 // Single-round fast path (payload = exactly G lines, 16-byte aligned; BASELINE config 1 is G = 8):
 // each step is one whole payload per lane-group, so there is no round state, and the per-lane line
 // pointer advances by a constant per task. Loads run one task ahead (A/B double buffer).
-template <int G, int BLK = kBlock>
+template <int G, int BLK = kBlock, int VWG = kVwg>
 __global__ __launch_bounds__(BLK) void crc32_oneround_kernel(const uint8_t* __restrict__ base, size_t n,
                                                                 size_t stride, const uint4* __restrict__ img_slice,
                                                                 const uint4* __restrict__ img_group,
@@ -268,7 +284,7 @@ __global__ __launch_bounds__(BLK) void crc32_oneround_kernel(const uint8_t* __re
   const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
 
   const uint32_t j = threadIdx.x & (G - 1);
-  const size_t gid = (blockIdx.x * (size_t)BLK + threadIdx.x) / G;
+  const size_t gid = group_id<BLK, G, VWG>();
   const size_t ngroups = ((size_t)gridDim.x * BLK) / G;
   const int ntasks = gid < n ? (int)((n - 1 - gid) / ngroups + 1) : 0;
   const size_t pstep = ngroups * stride;  // bytes between this group's consecutive payloads
@@ -378,7 +394,7 @@ __device__ __forceinline__ uint4 raw_task(size_t t, size_t end, const uint8_t* b
   }
 }
 
-template <int G, bool SORTED>
+template <int G, bool SORTED, int VWG = kVwg>
 __global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __restrict__ base, size_t n,
                                                            uint64_t fstride, uint32_t flen,
                                                            const uint4* __restrict__ desc,
@@ -392,7 +408,7 @@ __global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __rest
   const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
 
   const uint32_t j = threadIdx.x & (G - 1);
-  const size_t gid = (blockIdx.x * (size_t)kBlock + threadIdx.x) / G;
+  const size_t gid = group_id<kBlock, G, VWG>();
   const size_t ngroups = ((size_t)gridDim.x * kBlock) / G;
   const size_t t_begin = range ? range[0] : 0;
   const size_t t_end = range ? range[1] : n;
@@ -613,6 +629,59 @@ __global__ __launch_bounds__(kBucketBlock) void crc32_bucket_scatter(const uint8
   }
 }
 
+// ---- long payloads: segments + CRC combine ----
+// A batch of few long payloads cannot fill 256 CUs with at most 32 lanes per payload, and a batch
+// whose payload count is not a multiple of the lane-groups leaves a tail. Such payloads are cut into
+// segments aligned to their END (segment k of S ends at len - (S-1-k)*seg; segment 0 takes the
+// remainder), every segment is a task of the variable-length kernel, and the digests are joined with
+// the combine identity crc(A||B) = shift_|B|(crc A) ^ crc B folded over the segments:
+//   crc = XOR_k shift_{(S-1-k)*seg}(crc_k),
+// where every shift is a multiple of seg, so one table of powers serves the whole batch.
+__global__ __launch_bounds__(256) void crc32_split_desc(const uint8_t* __restrict__ base, size_t n, uint64_t len,
+                                                        uint64_t stride, uint64_t seg, uint32_t S,
+                                                        uint4* __restrict__ desc, uint32_t* __restrict__ range) {
+  const size_t total = n * (size_t)S;
+  for (size_t t = blockIdx.x * (size_t)256 + threadIdx.x; t < total; t += (size_t)gridDim.x * 256) {
+    const size_t i = t / S;
+    const uint32_t k = (uint32_t)(t - i * S);
+    const uint64_t end = len - (uint64_t)(S - 1 - k) * seg;
+    const uint64_t beg = k ? end - seg : 0;
+    const uint64_t a = (uint64_t)(uintptr_t)(base + i * stride + beg);
+    desc[t] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), (uint32_t)(end - beg), (uint32_t)t);
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    range[0] = 0;
+    range[1] = (uint32_t)total;
+  }
+}
+
+// One wave per payload; lane k applies shift_{(S-1-k)*seg} (32x32 GF(2) matrix, powers[(m-1)*32 + bit])
+// to segment k's digest, then the wave XOR-reduces.
+__global__ __launch_bounds__(256) void crc32_split_join(const uint32_t* __restrict__ seg_crc, size_t n, uint32_t S,
+                                                        const uint32_t* __restrict__ powers,
+                                                        uint32_t* __restrict__ out) {
+  const uint32_t lane = threadIdx.x & 63;
+  for (size_t i = blockIdx.x * (size_t)4 + (threadIdx.x >> 6); i < n; i += (size_t)gridDim.x * 4) {
+    uint32_t acc = 0;
+    for (uint32_t k = lane; k < S; k += 64) {
+      const uint32_t c = seg_crc[i * S + k];
+      const uint32_t m = S - 1 - k;
+      if (m == 0) {
+        acc ^= c;
+      } else {
+        const uint32_t* P = powers + (size_t)(m - 1) * 32;
+        uint32_t r = 0;
+#pragma unroll
+        for (int b = 0; b < 32; b++) r ^= P[b] & (0u - ((c >> b) & 1u));
+        acc ^= r;
+      }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) acc ^= __shfl_xor(acc, o, 64);
+    if (lane == 0) out[i] = acc;
+  }
+}
+
 template <int G>
 hipError_t launch_var_g(const VarLaunch& a, hipStream_t stream) {
   size_t blocks = a.max_blocks;
@@ -714,6 +783,22 @@ hipError_t launch_bucket(const void* base, size_t n, const uint64_t* d_off, cons
   hipLaunchKernelGGL(crc32_bucket_scan, dim3(1), dim3(kBuckets), 0, stream, rows, blocks, ranges);
   hipLaunchKernelGGL(crc32_bucket_scatter, dim3(blocks), dim3(kBucketBlock), 0, stream,
                      static_cast<const uint8_t*>(base), n, d_off, d_len, rows, static_cast<uint4*>(desc));
+  return hipGetLastError();
+}
+
+hipError_t launch_split_desc(const void* base, size_t n, uint64_t len, uint64_t stride, uint64_t seg, uint32_t S,
+                             void* desc, uint32_t* range, hipStream_t stream) {
+  const size_t total = n * (size_t)S;
+  const unsigned blocks = (unsigned)std::max<size_t>(1, std::min<size_t>(2048, (total + 255) / 256));
+  hipLaunchKernelGGL(crc32_split_desc, dim3(blocks), dim3(256), 0, stream, static_cast<const uint8_t*>(base), n, len,
+                     stride, seg, S, static_cast<uint4*>(desc), range);
+  return hipGetLastError();
+}
+
+hipError_t launch_split_join(const uint32_t* seg_crc, size_t n, uint32_t S, const uint32_t* powers, uint32_t* out,
+                             hipStream_t stream) {
+  const unsigned blocks = (unsigned)std::max<size_t>(1, std::min<size_t>(4096, (n + 3) / 4));
+  hipLaunchKernelGGL(crc32_split_join, dim3(blocks), dim3(256), 0, stream, seg_crc, n, S, powers, out);
   return hipGetLastError();
 }
 

@@ -1,6 +1,7 @@
-// A/B of product kernel variants on the headline workload (1M x 1 KiB): block size of the
-// single-round kernel. Includes the product source directly.
+// A/B of product kernel variants on the headline workload (1M x 1 KiB): virtual-workgroup mapping of
+// the single-round kernel (kVwg). Includes the product source directly.
 #include "../annety_amd/csrc/crc32_kernels.hip"
+#include "../annety_amd/csrc/crc32_frames.hip"
 #include "../annety_amd/csrc/crc32_capi.cpp"
 #include <cstdio>
 #include <vector>
@@ -44,9 +45,10 @@ int main() {
   for (int r = 0; r < 2000; r++) annety_crc32_batch_fixed(d, n, L, L, out, nullptr);
   for (int rep = 0; rep < 3; rep++) {
     b2b([&] { annety_crc32_batch_fixed(d, n, L, L, out, nullptr); }, "product (oneround<8,512>)");
-    b2b([&] { hipLaunchKernelGGL((crc32_oneround_kernel<8, 256>), dim3(256), dim3(256), 0, 0, (const uint8_t*)d, n, (size_t)L, (const uint4*)c->d_slice, (const uint4*)gimg, out); }, "oneround<8,256> grid256");
-    b2b([&] { hipLaunchKernelGGL((crc32_oneround_kernel<8, 1024>), dim3(256), dim3(1024), 0, 0, (const uint8_t*)d, n, (size_t)L, (const uint4*)c->d_slice, (const uint4*)gimg, out); }, "oneround<8,1024> grid256");
-    b2b([&] { hipLaunchKernelGGL((crc32_oneround_kernel<16, 512>), dim3(256), dim3(512), 0, 0, (const uint8_t*)d, n / 2, (size_t)2 * L, (const uint4*)c->d_slice, (const uint4*)group_image(*c, 16), out); }, "oneround<16,512> (2KiB payloads)");
+    b2b([&] { hipLaunchKernelGGL((crc32_oneround_kernel<8, 512, 0>), dim3(256), dim3(512), 0, 0, (const uint8_t*)d, n, (size_t)L, (const uint4*)c->d_slice, (const uint4*)gimg, out); }, "oneround<8,512> vwg off");
+    b2b([&] { hipLaunchKernelGGL((crc32_oneround_kernel<8, 512, 256>), dim3(256), dim3(512), 0, 0, (const uint8_t*)d, n, (size_t)L, (const uint4*)c->d_slice, (const uint4*)gimg, out); }, "oneround<8,512> vwg 256");
+    b2b([&] { hipLaunchKernelGGL((crc32_oneround_kernel<8, 512, 128>), dim3(256), dim3(512), 0, 0, (const uint8_t*)d, n, (size_t)L, (const uint4*)c->d_slice, (const uint4*)gimg, out); }, "oneround<8,512> vwg 128");
+    b2b([&] { hipLaunchKernelGGL((crc32_oneround_kernel<8, 512, 64>), dim3(256), dim3(512), 0, 0, (const uint8_t*)d, n, (size_t)L, (const uint4*)c->d_slice, (const uint4*)gimg, out); }, "oneround<8,512> vwg 64");
   }
   return 0;
 }
