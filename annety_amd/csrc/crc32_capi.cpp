@@ -317,10 +317,10 @@ uint64_t split_segment(size_t n, uint64_t len, int cus) {
   if (len < 2 * seg) return 0;
   const uint64_t S = (len + seg - 1) / seg;
   if ((uint64_t)n * S > 0xFFFFFFFFull) return 0;  // descriptor indices are 32-bit
-  (void)cus;
-  // auto == 1: splitting measured faster on every long-payload shape tried, from 1 x 1 GiB to
-  // 4096 x 4 MiB, so a payload of two or more segments is always split.
-  return seg;
+  // auto: whole payloads leave 32-lane groups idle (or a long tail) when there are fewer than two
+  // payloads per group; with more, whole payloads measured slightly faster.
+  const size_t groups_chip = (size_t)cus * fixed_kernel_block() / 32;
+  return n < 2 * groups_chip ? seg : 0;
 }
 
 // powers[(m-1)*32 + b] = shift_{m*seg}(1 << b) for m = 1..kMaxSegs-1, built once per segment size.

@@ -655,30 +655,39 @@ __global__ __launch_bounds__(256) void crc32_split_desc(const uint8_t* __restric
   }
 }
 
-// One wave per payload; lane k applies shift_{(S-1-k)*seg} (32x32 GF(2) matrix, powers[(m-1)*32 + bit])
-// to segment k's digest, then the wave XOR-reduces.
+// One wave per (payload, chunk of 64 segments); lane k applies shift_{(S-1-k)*seg} (32x32 GF(2)
+// matrix, powers[(m-1)*32 + bit]) to segment k's digest, the wave XOR-reduces, and a payload spread
+// over several chunks is accumulated with atomicXor (out pre-zeroed; XOR is order-independent, so the
+// result is deterministic). Every shift is absolute, so the chunks need no further join.
 __global__ __launch_bounds__(256) void crc32_split_join(const uint32_t* __restrict__ seg_crc, size_t n, uint32_t S,
                                                         const uint32_t* __restrict__ powers,
                                                         uint32_t* __restrict__ out) {
   const uint32_t lane = threadIdx.x & 63;
-  for (size_t i = blockIdx.x * (size_t)4 + (threadIdx.x >> 6); i < n; i += (size_t)gridDim.x * 4) {
+  const uint32_t chunks = (S + 63) / 64;
+  const size_t units = n * (size_t)chunks;
+  for (size_t u = blockIdx.x * (size_t)4 + (threadIdx.x >> 6); u < units; u += (size_t)gridDim.x * 4) {
+    const size_t i = u / chunks;
+    const uint32_t k = (uint32_t)(u - i * chunks) * 64 + lane;
     uint32_t acc = 0;
-    for (uint32_t k = lane; k < S; k += 64) {
+    if (k < S) {
       const uint32_t c = seg_crc[i * S + k];
       const uint32_t m = S - 1 - k;
       if (m == 0) {
-        acc ^= c;
+        acc = c;
       } else {
         const uint32_t* P = powers + (size_t)(m - 1) * 32;
-        uint32_t r = 0;
 #pragma unroll
-        for (int b = 0; b < 32; b++) r ^= P[b] & (0u - ((c >> b) & 1u));
-        acc ^= r;
+        for (int b = 0; b < 32; b++) acc ^= P[b] & (0u - ((c >> b) & 1u));
       }
     }
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) acc ^= __shfl_xor(acc, o, 64);
-    if (lane == 0) out[i] = acc;
+    if (lane == 0) {
+      if (chunks == 1)
+        out[i] = acc;
+      else
+        atomicXor(out + i, acc);
+    }
   }
 }
 
@@ -797,7 +806,12 @@ hipError_t launch_split_desc(const void* base, size_t n, uint64_t len, uint64_t 
 
 hipError_t launch_split_join(const uint32_t* seg_crc, size_t n, uint32_t S, const uint32_t* powers, uint32_t* out,
                              hipStream_t stream) {
-  const unsigned blocks = (unsigned)std::max<size_t>(1, std::min<size_t>(4096, (n + 3) / 4));
+  const size_t units = n * (size_t)((S + 63) / 64);
+  if (units > n) {
+    const hipError_t e = hipMemsetAsync(out, 0, n * sizeof(uint32_t), stream);
+    if (e != hipSuccess) return e;
+  }
+  const unsigned blocks = (unsigned)std::max<size_t>(1, std::min<size_t>(8192, (units + 3) / 4));
   hipLaunchKernelGGL(crc32_split_join, dim3(blocks), dim3(256), 0, stream, seg_crc, n, S, powers, out);
   return hipGetLastError();
 }

@@ -4,17 +4,10 @@
 set -e
 cd "$(dirname "$0")/.."
 run() { timeout -k 10 120 python bench.py --config 2 --payloads $1 --len $2 --steps 30 --warmup 5 --no-cpu --prewarm-s 0.5; }
-for shape in "4096 4194304" "1024 1048576" "16 67108864" "1 1073741824"; do
+for shape in "4096 4194304" "1024 1048576" "16 67108864" "1 1073741824" "1 268435456"; do
   set -- $shape
-  for seg in 16384 32768 65536 131072 262144; do
+  for seg in 32768 65536 131072; do
     echo "== n=$1 len=$2 split=1 seg=$seg"
     ANNETY_CRC_SPLIT=1 ANNETY_CRC_SEG=$seg run $1 $2
-  done
-done
-for shape in "65536 65536" "16384 262144" "32768 131072"; do
-  set -- $shape
-  for mode in 0 1; do
-    echo "== n=$1 len=$2 split=$mode"
-    ANNETY_CRC_SPLIT=$mode ANNETY_CRC_SEG=16384 run $1 $2
   done
 done
