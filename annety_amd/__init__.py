@@ -5,6 +5,8 @@ Public surface:
   crc32_batch             device-resident fixed-length batch   (C-ABI annety_crc32_batch_fixed)
   crc32_batch_var         device-resident variable-length batch (annety_crc32_batch_var)
   crc32_update_batch      raw-register batch update            (annety_crc32_update_batch_fixed)
+  crc32_update_batch_var  streaming update, one fragment/stream (annety_crc32_update_batch_var)
+  StreamingCrc            per-stream device registers over crc32_update_batch_var
   crc32_batch_host        host-memory batch, staged over PCIe  (annety_crc32_batch_fixed_host)
   crc32_combine           join two digests                     (annety_crc32_combine)
   LengthHeaderCodec       batched frame verify/build for annety's LengthHeaderCodec wire format
@@ -17,6 +19,8 @@ from .crc32c import (  # noqa: F401
     crc32_batch_var,
     crc32_combine,
     crc32_update_batch,
+    crc32_update_batch_var,
+    StreamingCrc,
     digests_to_numpy,
     tables,
 )
@@ -28,6 +32,8 @@ __all__ = [
     "crc32_batch",
     "crc32_batch_var",
     "crc32_update_batch",
+    "crc32_update_batch_var",
+    "StreamingCrc",
     "crc32_batch_host",
     "crc32_combine",
     "digests_to_numpy",

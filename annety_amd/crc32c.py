@@ -155,6 +155,48 @@ def crc32_update_batch(state, data, n: int, length: int, stride: Optional[int] =
     return state
 
 
+def crc32_update_batch_var(state, data, offsets, lengths, stream=None):
+    """Streaming update: state[i] (int32 device tensor, uint32 bit patterns) advanced in place over
+    fragment i = data[offsets[i] : offsets[i] + lengths[i]] (crc32_update semantics)."""
+    import torch
+
+    _require_device(data, "data")
+    _require_device(state, "state")
+    n = int(offsets.numel())
+    if offsets.dtype != torch.int64 or lengths.dtype != torch.int32 or lengths.numel() != n or state.numel() != n:
+        raise ValueError("offsets must be int64[n], lengths int32[n], state int32[n]")
+    st = _lib.get().annety_crc32_update_batch_var(_dev_ptr(state), _dev_ptr(data), _dev_ptr(offsets),
+                                                  _dev_ptr(lengths), n, _stream_handle(stream, state))
+    _lib.check(st, "annety_crc32_update_batch_var")
+    return state
+
+
+class StreamingCrc:
+    """Per-stream CRC registers on the device for payloads that arrive in fragments (one read_fd call
+    per connection at a time, src/TcpConnection.cc:445-448): seed 0xFFFFFFFF, crc32_update per
+    fragment, final xor - the reference's crc32_update protocol (include/Crc32c.h:71-82) batched over
+    streams."""
+
+    def __init__(self, n_streams: int, device=None):
+        import torch
+
+        self.state = torch.full((n_streams,), -1, dtype=torch.int32, device=device or "cuda")
+
+    def update(self, data, offsets, lengths, stream=None):
+        crc32_update_batch_var(self.state, data, offsets, lengths, stream)
+        return self
+
+    def digests(self):
+        """crc32_long of each stream's bytes so far (int32 device tensor of uint32 bit patterns)."""
+        return self.state ^ -1
+
+    def reset(self, mask=None):
+        if mask is None:
+            self.state.fill_(-1)
+        else:
+            self.state[mask] = -1
+
+
 def crc32_batch_host(buf: BytesLike, n: int, length: int, stride: Optional[int] = None) -> np.ndarray:
     """Host-memory batch: staged to the current device and back (synchronous). Returns uint32[n]."""
     stride = length if stride is None else stride

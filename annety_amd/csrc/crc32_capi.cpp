@@ -245,8 +245,9 @@ int run_fixed(DeviceCtx& c, const void* d_base, size_t n, size_t len, size_t str
 }
 
 int run_var(DeviceCtx& c, const void* d_base, size_t n, uint64_t fstride, uint32_t flen, uint32_t group,
-            const void* desc, const uint32_t* range, uint32_t* d_out, hipStream_t stream) {
+            const void* desc, const uint32_t* range, uint32_t* d_out, hipStream_t stream, bool update = false) {
   VarLaunch a{};
+  a.update = update;
   a.base = d_base;
   a.n = n;
   a.fixed_stride = fstride;
@@ -267,7 +268,7 @@ int run_var(DeviceCtx& c, const void* d_base, size_t n, uint64_t fstride, uint32
 // Variable batch: bucket by line count on the device (no host round trip), then one launch per
 // length class with its own lane-group width. Scratch comes from the stream-ordered allocator.
 int run_var_sorted(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_off, const uint32_t* d_len,
-                   uint32_t* d_out, hipStream_t stream) {
+                   uint32_t* d_out, hipStream_t stream, bool update = false) {
   const size_t rows_words = (size_t)bucket_blocks(n) * bucket_count();
   const size_t head = (rows_words + 8) * sizeof(uint32_t);  // rows + ranges (16-byte multiple)
   char* scratch = nullptr;
@@ -276,11 +277,11 @@ int run_var_sorted(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d
   uint32_t* ranges = rows + rows_words;
   void* desc = scratch + head;
   int rc = ANNETY_CRC_OK;
-  hipError_t e = launch_bucket(d_base, n, d_off, d_len, rows, ranges, desc, d_out, stream);
+  hipError_t e = launch_bucket(d_base, n, d_off, d_len, rows, ranges, desc, update ? nullptr : d_out, stream);
   if (e != hipSuccess) rc = hip_fail(e);
   const uint32_t groups[3] = {32, 8, 2};
   for (int k = 0; k < 3 && rc == ANNETY_CRC_OK; k++)
-    rc = run_var(c, d_base, n, 0, 0, groups[k], desc, ranges + 2 * k, d_out, stream);
+    rc = run_var(c, d_base, n, 0, 0, groups[k], desc, ranges + 2 * k, d_out, stream, update);
   e = hipFreeAsync(scratch, stream);
   if (rc == ANNETY_CRC_OK && e != hipSuccess) rc = hip_fail(e);
   return rc;
@@ -525,11 +526,26 @@ int annety_crc32_update_batch_fixed(uint32_t* d_state, const void* d_base, size_
                                     void* stream) {
   if (n == 0 || len == 0) return ANNETY_CRC_OK;  // no bytes: register unchanged
   if (!d_state || !d_base || (n > 1 && stride < len)) return ANNETY_CRC_EINVAL;
-  if (!fixed_fast_ok(d_base, len, stride)) return ANNETY_CRC_EINVAL;  // raw path needs the aligned layout
+  if (len > 0xFFFFFFFFull) return ANNETY_CRC_EINVAL;
   DeviceCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
-  return run_fixed(*c, d_base, n, len, stride, d_state, true, static_cast<hipStream_t>(stream));
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  if (fixed_fast_ok(d_base, len, stride)) return run_fixed(*c, d_base, n, len, stride, d_state, true, s);
+  const uint64_t lines = (len + 255) / 128;  // odd shapes: the general kernel in update mode
+  return run_var(*c, d_base, n, stride, (uint32_t)len, pick_group(lines, n, c->cus), nullptr, nullptr, d_state, s,
+                 true);
+}
+
+int annety_crc32_update_batch_var(uint32_t* d_state, const void* d_base, const uint64_t* d_off, const uint32_t* d_len,
+                                  size_t n, void* stream) {
+  if (n == 0) return ANNETY_CRC_OK;
+  if (!d_state || !d_base || !d_off || !d_len) return ANNETY_CRC_EINVAL;
+  if (n > 0xFFFFFFFFull) return ANNETY_CRC_EINVAL;
+  DeviceCtx* c = nullptr;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  return run_var_sorted(*c, d_base, n, d_off, d_len, d_state, static_cast<hipStream_t>(stream), true);
 }
 
 int annety_crc32_batch_fixed_host(const void* h_base, size_t n, size_t len, size_t stride, uint32_t* h_out) {

@@ -42,15 +42,16 @@ struct VarLaunch {
   const void* img_group;
   const void* img_unshift;   // 12 KiB two-level inverse-shift tables (LDS image part 3)
   const uint32_t* short_init;  // shift_len(0xFFFFFFFF) for len = 0..3
-  uint32_t* out;
+  uint32_t* out;             // digests, or (update) the register array, read and written in place
   size_t max_blocks;
+  bool update;               // crc32_update semantics instead of crc32_long
 };
 
 hipError_t launch_var(const VarLaunch& a, hipStream_t stream);
 
 // Counting sort of a variable batch by 128-byte line count (longest first): writes desc[] (16 B per
 // non-empty payload), ranges[6] = {begin,end} of the G=32 / G=8 / G=2 classes, and out[p] = 0 for
-// zero-length payloads. Scratch: rows = bucket_blocks(n) * bucket_count() words, ranges = 8 words,
+// zero-length payloads (out may be null: update mode leaves their registers alone). Scratch: rows = bucket_blocks(n) * bucket_count() words, ranges = 8 words,
 // desc = 16*n bytes.
 hipError_t launch_bucket(const void* base, size_t n, const uint64_t* d_off, const uint32_t* d_len, uint32_t* rows,
                          uint32_t* ranges, void* desc, uint32_t* out, hipStream_t stream);

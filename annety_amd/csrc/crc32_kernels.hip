@@ -345,6 +345,7 @@ __global__ __launch_bounds__(BLK) void crc32_oneround_kernel(const uint8_t* __re
 struct VarTask {
   uint64_t line0;    // absolute index of the payload's first 128-byte line
   uint32_t nlines, rounds, vlead, lead, tailend, len, p;
+  uint32_t state;    // update mode: the register before this payload (crc32_update semantics)
   bool valid;
 };
 
@@ -394,7 +395,11 @@ __device__ __forceinline__ uint4 raw_task(size_t t, size_t end, const uint8_t* b
   }
 }
 
-template <int G, bool SORTED, int VWG = kVwg>
+//   UPD: crc32_update semantics (include/Crc32c.h:71-82): out[p] holds the register before payload p on
+//        entry and after it on exit (no init, no final xor). The entry register s is injected like the
+//        init: raw(M, s) = raw(M ^ (s as payload bytes 0..3, little-endian), 0) when len >= 4, and
+//        shift_len(s) ^ raw(M, 0) below that.
+template <int G, bool SORTED, bool UPD = false, int VWG = kVwg>
 __global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __restrict__ base, size_t n,
                                                            uint64_t fstride, uint32_t flen,
                                                            const uint4* __restrict__ desc,
@@ -436,6 +441,7 @@ __global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __rest
   //          fetches   the raw descriptor of step q+2's task.
   size_t t0 = t_begin + gid;
   VarTask dec0 = decode_task<G>(raw(t0), t0 < t_end);
+  if constexpr (UPD) dec0.state = dec0.valid ? out[dec0.p] : 0u;
   uint32_t r0 = 0;
   size_t t1 = dec0.rounds > 1 ? t0 : t0 + ngroups;
   uint32_t r1 = dec0.rounds > 1 ? 1u : 0u;
@@ -463,16 +469,34 @@ __global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __rest
       const bool spill = li == 1 && cur.lead > 124 && cur.len >= 4;
       if (first || spill) {
         const int32_t A8 = first ? (int32_t)cur.lead * 8 : 0;
-        const int32_t B8 = cur.len < 4 ? A8 : ((int32_t)cur.lead + 4 - (first ? 0 : 128)) * 8;
+        if constexpr (UPD) {
+          // the register's bytes land at payload bytes 0..3, i.e. line bit offset S8 (< 0 on the spill line)
+          const int32_t S8 = ((int32_t)cur.lead - (first ? 0 : 128)) * 8;
+          const uint32_t reg = cur.len < 4 ? 0u : cur.state;
 #pragma unroll
-        for (int i = 0; i < 8; i++) {
-          uint32_t* w = reinterpret_cast<uint32_t*>(&v[i]);
+          for (int i = 0; i < 8; i++) {
+            uint32_t* w = reinterpret_cast<uint32_t*>(&v[i]);
 #pragma unroll
-          for (int q = 0; q < 4; q++) {
-            const int32_t p8 = (i * 16 + q * 4) * 8;
-            const uint32_t keepA = (uint32_t)(0xFFFFFFFFull << clamp032(A8 - p8));
-            const uint32_t keepB = (uint32_t)(0xFFFFFFFFull << clamp032(B8 - p8));
-            w[q] = keepA & (w[q] ^ ~keepB);
+            for (int q = 0; q < 4; q++) {
+              const int32_t p8 = (i * 16 + q * 4) * 8;
+              const uint32_t keepA = (uint32_t)(0xFFFFFFFFull << clamp032(A8 - p8));
+              const int32_t x = S8 - p8;  // bit offset of register byte 0 inside this word
+              const uint32_t sw = x >= 32 || x <= -32 ? 0u : (x >= 0 ? reg << x : reg >> -x);
+              w[q] = (keepA & w[q]) ^ sw;
+            }
+          }
+        } else {
+          const int32_t B8 = cur.len < 4 ? A8 : ((int32_t)cur.lead + 4 - (first ? 0 : 128)) * 8;
+#pragma unroll
+          for (int i = 0; i < 8; i++) {
+            uint32_t* w = reinterpret_cast<uint32_t*>(&v[i]);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+              const int32_t p8 = (i * 16 + q * 4) * 8;
+              const uint32_t keepA = (uint32_t)(0xFFFFFFFFull << clamp032(A8 - p8));
+              const uint32_t keepB = (uint32_t)(0xFFFFFFFFull << clamp032(B8 - p8));
+              w[q] = keepA & (w[q] ^ ~keepB);
+            }
           }
         }
       }
@@ -499,18 +523,24 @@ __global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __rest
           t = nibble_map_uniform(t, lds, kLdsUnshiftOff + (over & 15u) * 512);
           t = nibble_map_uniform(t, lds, kLdsUnshiftOff + 8192 + (over >> 4) * 512);
         }
-        if (cur.len < 4) {  // shift_len(0xFFFFFFFF): init not expressible as a complement (constants)
-          constexpr uint32_t k1 = shift_bits(kInit, 8), k2 = shift_bits(kInit, 16), k3 = shift_bits(kInit, 24);
-          t ^= cur.len == 1 ? k1 : (cur.len == 2 ? k2 : k3);
+        if constexpr (UPD) {
+          if (cur.len < 4) t ^= shift_bits(cur.state, 8u * cur.len);  // <= 24 bit steps
+          out[cur.p] = t;
+        } else {
+          if (cur.len < 4) {  // shift_len(0xFFFFFFFF): init not expressible as a complement (constants)
+            constexpr uint32_t k1 = shift_bits(kInit, 8), k2 = shift_bits(kInit, 16), k3 = shift_bits(kInit, 24);
+            t ^= cur.len == 1 ? k1 : (cur.len == 2 ? k2 : k3);
+          }
+          out[cur.p] = ~t;
         }
-        out[cur.p] = ~t;
       }
       s = 0;
     }
   };
 
   auto step = [&](uint4 (&cur_buf)[8], uint4 (&nxt_buf)[8]) {
-    const VarTask dec1 = decode_task<G>(d1, t1 < t_end);
+    VarTask dec1 = decode_task<G>(d1, t1 < t_end);
+    if constexpr (UPD) dec1.state = dec1.valid ? out[dec1.p] : 0u;  // read one step before it is used
     const bool more = r1 + 1 < dec1.rounds;
     const size_t t2 = more ? t1 : t1 + ngroups;
     const uint32_t r2 = more ? r1 + 1 : 0u;
@@ -564,7 +594,7 @@ __global__ __launch_bounds__(kBucketBlock) void crc32_bucket_hist(const uint8_t*
   for (size_t p = lo + threadIdx.x; p < hi; p += kBucketBlock) {
     const uint32_t len = d_len[p];
     if (len == 0) {
-      out[p] = 0u;  // crc of the empty string
+      if (out) out[p] = 0u;  // crc of the empty string (update mode: the register is unchanged)
       continue;
     }
     atomicAdd(&h[bucket_of((uint64_t)(uintptr_t)(base + d_off[p]), len)], 1u);
@@ -699,18 +729,20 @@ hipError_t launch_var_g(const VarLaunch& a, hipStream_t stream) {
     blocks = std::min(blocks, (lanes + kBlock - 1) / kBlock);
   }
   if (blocks == 0) return hipSuccess;
-  if (a.desc)
-    hipLaunchKernelGGL((crc32_var_kernel<G, true>), dim3((unsigned)blocks), dim3(kBlock), 0, stream,
-                       static_cast<const uint8_t*>(a.base), a.n, a.fixed_stride, a.fixed_len,
-                       static_cast<const uint4*>(a.desc), a.range, static_cast<const uint4*>(a.img_slice),
-                       static_cast<const uint4*>(a.img_group), static_cast<const uint4*>(a.img_unshift), a.short_init,
-                       a.out);
-  else
-    hipLaunchKernelGGL((crc32_var_kernel<G, false>), dim3((unsigned)blocks), dim3(kBlock), 0, stream,
-                       static_cast<const uint8_t*>(a.base), a.n, a.fixed_stride, a.fixed_len,
-                       static_cast<const uint4*>(a.desc), a.range, static_cast<const uint4*>(a.img_slice),
-                       static_cast<const uint4*>(a.img_group), static_cast<const uint4*>(a.img_unshift), a.short_init,
-                       a.out);
+#define ANNETY_VAR_LAUNCH(SORTED, UPD)                                                                     \
+  hipLaunchKernelGGL((crc32_var_kernel<G, SORTED, UPD>), dim3((unsigned)blocks), dim3(kBlock), 0, stream,   \
+                     static_cast<const uint8_t*>(a.base), a.n, a.fixed_stride, a.fixed_len,                  \
+                     static_cast<const uint4*>(a.desc), a.range, static_cast<const uint4*>(a.img_slice),     \
+                     static_cast<const uint4*>(a.img_group), static_cast<const uint4*>(a.img_unshift),       \
+                     a.short_init, a.out)
+  if (a.desc) {
+    if (a.update) ANNETY_VAR_LAUNCH(true, true);
+    else ANNETY_VAR_LAUNCH(true, false);
+  } else {
+    if (a.update) ANNETY_VAR_LAUNCH(false, true);
+    else ANNETY_VAR_LAUNCH(false, false);
+  }
+#undef ANNETY_VAR_LAUNCH
   return hipGetLastError();
 }
 

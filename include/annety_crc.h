@@ -72,9 +72,15 @@ int annety_crc32_batch_fixed(const void* d_base, size_t n, size_t len, size_t st
 int annety_crc32_batch_var(const void* d_base, const uint64_t* d_off, const uint32_t* d_len, size_t n,
                            uint32_t* d_out, void* stream);
 /* Raw-register update (crc32_update semantics) for a fixed-length batch: d_state[i] is the register
- * before payload i on input and after it on output (no init, no final xor). */
+ * before payload i on input and after it on output (no init, no final xor). Any alignment. */
 int annety_crc32_update_batch_fixed(uint32_t* d_state, const void* d_base, size_t n, size_t len, size_t stride,
                                     void* stream);
+/* Streaming update: one fragment per stream, fragment i = [d_base + d_off[i],
+ * + d_len[i]) advances stream i's register d_state[i] in place (crc32_update, include/Crc32c.h:71-82).
+ * A fragment of length 0 leaves its register unchanged. Seed with 0xFFFFFFFF and xor the final register
+ * with 0xFFFFFFFF to get crc32_long of the whole stream. */
+int annety_crc32_update_batch_var(uint32_t* d_state, const void* d_base, const uint64_t* d_off, const uint32_t* d_len,
+                                  size_t n, void* stream);
 
 /* ---- host-memory batch (payloads off a NetBuffer/socket): staged through pinned buffers, H2D ->
  * kernel -> D2H, pipelined on two streams. Synchronous. ---- */

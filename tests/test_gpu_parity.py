@@ -218,3 +218,66 @@ def test_config1_properties(config1):
     joined = np.array([oracle.crc32_combine(int(base[2 * i]), int(base[2 * i + 1]), L) for i in range(0, n // 2, 509)],
                       dtype=np.uint32)
     assert np.array_equal(pairs[::509], joined)
+
+
+def test_update_batch_var(gpu):
+    """Streaming update (§8f row 4): arbitrary registers, unaligned fragments of every length class,
+    including the < 4-byte fragments whose register cannot be injected as payload bytes."""
+    import annety_amd
+    import torch
+
+    rng = np.random.default_rng(77)
+    n = 6000
+    lens = np.concatenate([np.arange(0, 300), rng.integers(0, 5000, n - 400), rng.integers(16384, 70000, 100)])
+    rng.shuffle(lens)
+    offs = np.cumsum(np.concatenate([[0], lens[:-1] + rng.integers(0, 7, n - 1)])).astype(np.int64)
+    arena = oracle.lcg_bytes(int(offs[-1] + lens[-1]) + 16, 404)
+    states = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+    d_state = to_dev(states.view(np.int32), gpu)
+    annety_amd.crc32_update_batch_var(d_state, to_dev(arena, gpu), to_dev(offs, gpu),
+                                      to_dev(lens.astype(np.int32), gpu))
+    got = digests(d_state)
+    want = np.array([oracle.crc32_update(int(s), arena[o : o + L]) for s, o, L in zip(states, offs, lens)],
+                    dtype=np.uint32)
+    assert np.array_equal(got, want)
+
+
+def test_streaming_fragments(gpu):
+    """Streams delivered in random fragments over several calls end at crc32_long of the whole."""
+    import annety_amd
+    import torch
+
+    rng = np.random.default_rng(78)
+    ns = 500
+    total = rng.integers(0, 40000, ns)
+    bodies = [oracle.lcg_bytes(int(t), 1000 + i) for i, t in enumerate(total)]
+    cuts = [np.sort(rng.integers(0, int(t) + 1, 4)) for t in total]
+    sc = annety_amd.StreamingCrc(ns, gpu)
+    for call in range(5):
+        frags = []
+        for i in range(ns):
+            edges = np.concatenate([[0], cuts[i], [total[i]]])
+            frags.append(bodies[i][edges[call] : edges[call + 1]])
+        lens = np.array([f.size for f in frags], dtype=np.int32)
+        offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+        arena = np.concatenate(frags + [np.zeros(1, np.uint8)])
+        sc.update(to_dev(arena, gpu), to_dev(offs, gpu), to_dev(lens, gpu))
+    got = digests(sc.digests())
+    want = np.array([oracle.crc32_long(b) for b in bodies], dtype=np.uint32)
+    assert np.array_equal(got, want)
+
+
+def test_update_batch_fixed_odd_shapes(gpu):
+    """Raw update over shapes the aligned kernel does not take (general kernel, update mode)."""
+    import annety_amd
+    import torch
+
+    rng = np.random.default_rng(79)
+    host = oracle.lcg_bytes(1 << 20, 55)
+    d = to_dev(host, gpu)
+    for n, L, stride, off in [(100, 1000, 1003, 1), (7, 3, 5, 2), (33, 4097, 4097, 0), (5, 100000, 100001, 3)]:
+        states = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32)
+        d_state = to_dev(states.view(np.int32), gpu)
+        annety_amd.crc32_update_batch(d_state, d[off:], n, L, stride)
+        want = [oracle.crc32_update(int(states[i]), host[off + i * stride : off + i * stride + L]) for i in range(n)]
+        assert [int(x) for x in digests(d_state)] == want, (n, L, stride, off)
