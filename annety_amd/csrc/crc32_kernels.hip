@@ -399,7 +399,9 @@ __device__ __forceinline__ uint4 raw_task(size_t t, size_t end, const uint8_t* b
 //        entry and after it on exit (no init, no final xor). The entry register s is injected like the
 //        init: raw(M, s) = raw(M ^ (s as payload bytes 0..3, little-endian), 0) when len >= 4, and
 //        shift_len(s) ^ raw(M, 0) below that.
-template <int G, bool SORTED, bool UPD = false, int VWG = kVwg>
+//   PROBE (microbench only; product = 0): bit 0 drops the byte masks, bit 1 the unshift - wrong
+//        digests, used to measure what those stages cost (microbench/ab3.hip).
+template <int G, bool SORTED, bool UPD = false, int VWG = kVwg, int PROBE = 0>
 __global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __restrict__ base, size_t n,
                                                            uint64_t fstride, uint32_t flen,
                                                            const uint4* __restrict__ desc,
@@ -467,7 +469,7 @@ __global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __rest
       //   tail side: keep bytes < hi                            -> w &= keepH
       const bool first = li == 0, last = (uint32_t)li == cur.nlines - 1;
       const bool spill = li == 1 && cur.lead > 124 && cur.len >= 4;
-      if (first || spill) {
+      if ((PROBE & 1) == 0 && (first || spill)) {
         const int32_t A8 = first ? (int32_t)cur.lead * 8 : 0;
         if constexpr (UPD) {
           // the register's bytes land at payload bytes 0..3, i.e. line bit offset S8 (< 0 on the spill line)
@@ -500,7 +502,7 @@ __global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __rest
           }
         }
       }
-      if (last) {
+      if ((PROBE & 1) == 0 && last) {
         const int32_t H8 = (int32_t)cur.tailend * 8;
 #pragma unroll
         for (int i = 0; i < 8; i++) {
@@ -519,7 +521,7 @@ __global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __rest
       if constexpr (G > 1) t = group_xor_reduce<G>(nibble_map_lane(s, lds, k.slot4));
       if (cur.valid && j == G - 1) {
         const uint32_t over = 128 - cur.tailend;  // trailing zero bytes of the last line
-        if (over) {  // shift_{-over} = U_hi[over >> 4] o U_lo[over & 15], both from LDS
+        if ((PROBE & 2) == 0 && over) {  // shift_{-over} = U_hi[over >> 4] o U_lo[over & 15], both from LDS
           t = nibble_map_uniform(t, lds, kLdsUnshiftOff + (over & 15u) * 512);
           t = nibble_map_uniform(t, lds, kLdsUnshiftOff + 8192 + (over >> 4) * 512);
         }
