@@ -15,4 +15,5 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-include-regex crc32_ --out
   python3 $R/bench.py --steps 10 --warmup 2 --prewarm-s 0.3 --no-cpu > $OUT/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-include-regex crc32_ --output-format csv -d $OUT/write -o run -- \
   python3 $R/bench.py --steps 10 --warmup 2 --prewarm-s 0.3 --no-cpu > $OUT/write.log 2>&1
-python3 $R/profiles/parse_prof.py $OUT $TAG
+# summaries are written locally after gpurun merges gpurun_out/ back:
+#   python3 profiles/parse_prof.py gpurun_out/prof_<tag> <tag>
