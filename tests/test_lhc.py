@@ -5,11 +5,15 @@ LengthHeaderCodec (tests/golden/lhc.json, tests/golden/make_lhc_golden.py) and c
 of the C-ABI (header walk, encode plan, recv outcome). GPU tests run decode/encode through the C-ABI
 and compare with the fixtures and the oracle.
 """
+import os
+
 import numpy as np
 import pytest
 
 import oracle
 from annety_amd.codec import LengthHeaderCodec, recv_result
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _payload(n, seed):
@@ -154,3 +158,147 @@ def test_gpu_encode_decode_round_trip_and_corruption(gpu):
         e = codec.decode_batch(bytes(bad), device=gpu)
         assert e.rt == -1 and e.payload_off.size == k and e.consumed == int(d.payload_off[k]) - T
         assert int((e.ok == 0).sum()) == 1
+
+
+# ---------------- the reference codec itself, linked against the drop-in ----------------
+@pytest.mark.skipif(not os.path.isdir("/root/reference/src"), reason="reference tree not present")
+def test_reference_codec_runs_on_dropin(golden, tmp_path):
+    """annety's own LengthHeaderCodec (include/codec/LengthHeaderCodec.h) compiled with the drop-in
+    Crc32c.h first on the include path and linked with libannety_crc.so in place of src/Crc32c.cc
+     reproduces every recorded encode output and decode sequence."""
+    import ctypes
+    import glob
+    import subprocess
+
+    from annety_amd import _lib
+
+    oracle.build(ref=True)
+    objs = [o for o in glob.glob(os.path.join(ROOT, "oracle", "_ref", "obj", "*.o"))
+            if os.path.basename(o) != "Crc32c.o"]
+    assert len(objs) > 40
+    so = tmp_path / "libdropin_codec.so"
+    libdir = os.path.dirname(_lib.lib_path())
+    subprocess.run(["g++", "-std=c++11", "-O2", "-fPIC", "-shared", "-w", "-include", "functional",
+                    f"-I{ROOT}/include/annety", f"-I{ROOT}/include", "-I/root/reference/include",
+                    "-I/root/reference/src", os.path.join(ROOT, "oracle", "ref_codec.cc"), *objs, "-o", str(so),
+                    f"-L{libdir}", "-lannety_crc", f"-Wl,-rpath,{libdir}", "-lpthread"], check=True)
+    # the tables must come from the engine library, not from a stray copy of src/Crc32c.cc
+    nm = subprocess.run(["nm", "-D", "--defined-only", str(so)], capture_output=True, text=True).stdout
+    assert "_ZN6annety8internal14crc32_table256E" not in nm
+    lib = ctypes.CDLL(str(so))
+    sp = ctypes.POINTER(ctypes.c_size_t)
+    lib.ref_lhc_encode.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                   ctypes.c_size_t, sp]
+    lib.ref_lhc_decode.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+                                   ctypes.c_size_t, sp, sp]
+    g = golden("lhc.json")
+    for c in g["encode"]:
+        p = _payload(c["len"], c["seed"])
+        out = ctypes.create_string_buffer(len(p) + 16)
+        n = ctypes.c_size_t()
+        rt = lib.ref_lhc_encode(c["T"], c["max_payload"], p, len(p), out, len(p) + 16, ctypes.byref(n))
+        assert rt == c["rt"] and out.raw[: n.value] == _expected_encode(c), c
+    for c in g["decode"]:
+        s = bytes.fromhex(c["stream"])
+        frames, pos = [], 0
+        while True:
+            rest = s[pos:]
+            buf = ctypes.create_string_buffer(len(rest) + 1)
+            pl, used = ctypes.c_size_t(), ctypes.c_size_t()
+            rt = lib.ref_lhc_decode(c["T"], c["max_payload"], rest, len(rest), buf, len(rest) + 1, ctypes.byref(pl),
+                                    ctypes.byref(used))
+            if rt != 1:
+                break
+            frames.append([pos + c["T"], pl.value])
+            pos += used.value
+        assert frames == c["frames"] and (pos, rt) == (c["consumed"], c["rt"]), c["name"]
+
+
+CPP_BATCH = r"""
+// Host side of include/annety/LengthHeaderCodecBatch.h (no device calls): locate + recv_outcome with
+// verdicts from the drop-in's host Crc32c, and plan. Reads a stream file, prints what recv would do.
+#define ANNETY_CRC_NO_STRINGPIECE
+#include "annety/Crc32c.h"
+#include "annety/LengthHeaderCodecBatch.h"
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+int main(int argc, char** argv) {
+  if (argc != 4) return 1;
+  const int T = std::atoi(argv[2]);
+  const long long maxp = std::atoll(argv[3]);
+  std::FILE* f = std::fopen(argv[1], "rb");
+  std::vector<char> buf;
+  int ch;
+  while ((ch = std::fgetc(f)) != EOF) buf.push_back((char)ch);
+  std::fclose(f);
+  annety::LengthHeaderCodecBatch codec((annety::LengthHeaderCodecBatch::LENGTH_TYPE)T, maxp);
+  annety::LengthHeaderCodecBatch::Frames fr;
+  if (codec.locate(buf.data(), buf.size(), &fr) != 0) return 2;
+  std::vector<uint8_t> ok(fr.payload_off.size());
+  for (size_t i = 0; i < ok.size(); i++) {
+    const unsigned char* t = reinterpret_cast<const unsigned char*>(buf.data() + fr.payload_off[i] + fr.payload_len[i]);
+    const uint32_t want = (uint32_t)t[0] << 24 | (uint32_t)t[1] << 16 | (uint32_t)t[2] << 8 | t[3];
+    ok[i] = annety::Crc32c::crc32_long(buf.data() + fr.payload_off[i], fr.payload_len[i]) == want;
+  }
+  size_t delivered = 0, consumed = 0;
+  const int rt = codec.recv_outcome(fr, ok.data(), &delivered, &consumed);
+  std::printf("%d %zu %zu", rt, delivered, consumed);
+  for (size_t i = 0; i < delivered; i++) std::printf(" %llu:%u", (unsigned long long)fr.payload_off[i], fr.payload_len[i]);
+  std::printf("\n");
+  // plan over the payload lengths found (+ an empty one and one above max_payload when it is set)
+  std::vector<uint32_t> lens(fr.payload_len.begin(), fr.payload_len.end());
+  lens.push_back(0);
+  if (maxp > 0) lens.push_back((uint32_t)maxp + 1);
+  std::vector<uint64_t> off(lens.size());
+  std::vector<int8_t> prt(lens.size());
+  uint64_t total = 0;
+  if (codec.plan(lens.data(), lens.size(), off.data(), prt.data(), &total) != 0) return 3;
+  std::printf("%llu", (unsigned long long)total);
+  for (size_t i = 0; i < lens.size(); i++) std::printf(" %d:%llu", prt[i], (unsigned long long)off[i]);
+  std::printf("\n");
+  return 0;
+}
+"""
+
+
+def test_cpp_batch_codec_host_side(golden, tmp_path):
+    """The C++ batch codec's host logic equals Codec::recv on the reference-recorded streams and on
+    long generated ones; its plan() equals encode()'s decisions."""
+    import subprocess
+
+    from annety_amd import _lib
+
+    src = tmp_path / "b.cc"
+    src.write_text(CPP_BATCH)
+    exe = tmp_path / "b"
+    libdir = os.path.dirname(_lib.lib_path())
+    subprocess.run(["g++", "-std=c++11", "-O2", "-Wall", "-Wextra", "-Werror", f"-I{ROOT}/include", str(src), "-o",
+                    str(exe), f"-L{libdir}", "-lannety_crc", f"-Wl,-rpath,{libdir}"], check=True)
+    cases = [(c["T"], c["max_payload"], bytes.fromhex(c["stream"])) for c in golden("lhc.json")["decode"]]
+    rng = np.random.default_rng(9)
+    for T in (1, 2, 4, 8):
+        lens = rng.integers(0, 120 if T == 1 else 3000, 300)
+        s = b"".join(oracle.lhc_encode(_payload(int(n), i), T)[1] for i, n in enumerate(lens))
+        bad = bytearray(s)
+        bad[len(s) // 2] ^= 1
+        cases += [(T, 1 << 26, s), (T, 1 << 26, s[:-7]), (T, 1 << 26, bytes(bad)), (T, 500, s)]
+    for T, maxp, s in cases:
+        f = tmp_path / "s.bin"
+        f.write_bytes(s)
+        out = subprocess.run([str(exe), str(f), str(T), str(maxp)], capture_output=True, text=True, check=True)
+        line1, line2 = out.stdout.strip().split("\n")
+        head = line1.split()
+        frames, used, rt = oracle.lhc_recv(s, T, maxp)
+        assert int(head[0]) == rt and int(head[1]) == len(frames) and int(head[2]) == used
+        assert [tuple(map(int, x.split(":"))) for x in head[3:]] == [tuple(x) for x in frames]
+        plan = line2.split()
+        lens = [n for _, n in frames] if rt == 0 else None
+        if lens is not None:
+            pos, want = 0, []
+            for n in lens + [0] + ([maxp + 1] if maxp > 0 else []):
+                r = 0 if n == 0 else (-1 if maxp > 0 and n > maxp else 1)
+                want.append(f"{r}:{pos}")
+                pos += T + n + 4 if r == 1 else 0
+            assert plan[1:] == want and int(plan[0]) == pos
