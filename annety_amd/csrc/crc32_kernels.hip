@@ -48,25 +48,11 @@ struct LaneCtx {
   uint32_t slot4;  // replica*4 for the 4-byte join tables
 };
 
-// Absorb one 32-bit word. x = register ^ word (little-endian bytes b0..b3). Returns
-// T3[b0]^T2[b1]^T1[b2]^T0[b3] ^ wnext, i.e. the register after the word, pre-xored with the next word.
-// The four ds_read_b64 are issued back-to-back through inline asm so the compiler cannot narrow them to
-// ds_read_b32 (which would use the 32-bank rule and conflict 2-way); the wait is tied to the results.
-__device__ __forceinline__ uint32_t word4(uint32_t x, uint32_t wnext, const LaneCtx& k) {
-  const uint32_t a0 = __builtin_amdgcn_perm(x, k.L0, 0x0C020400u);
-  const uint32_t a1 = __builtin_amdgcn_perm(x, k.L0, 0x0C020500u);
-  const uint32_t a2 = __builtin_amdgcn_perm(x, k.L1, 0x0C020600u);
-  const uint32_t a3 = __builtin_amdgcn_perm(x, k.L1, 0x0C020700u);
-  uint2 v0, v1, v2, v3;
-  asm volatile("ds_read_b64 %0, %1" : "=v"(v0) : "v"(a0));
-  asm volatile("ds_read_b64 %0, %1" : "=v"(v1) : "v"(a1));
-  asm volatile("ds_read_b64 %0, %1" : "=v"(v2) : "v"(a2));
-  asm volatile("ds_read_b64 %0, %1" : "=v"(v3) : "v"(a3));
-  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3));
-  return xor3(xor3(v0.x, v1.y, v2.x), v3.y, wnext);
-}
-
-// Two independent words at once (two chains): 8 address perms, 8 ds_read_b64 in flight, one wait.
+// Absorb one 32-bit word per chain, two chains at once. x = register ^ word (little-endian bytes
+// b0..b3) becomes T3[b0]^T2[b1]^T1[b2]^T0[b3] ^ wnext, i.e. the register after the word, pre-xored with
+// the chain's next word. The eight ds_read_b64 are issued back-to-back through inline asm so the
+// compiler cannot narrow them to ds_read_b32 (which would use the 32-bank rule and conflict 2-way);
+// the single wait is tied to the results.
 __device__ __forceinline__ void word4x2(uint32_t& xa, uint32_t wa, uint32_t& xb, uint32_t wb, const LaneCtx& k) {
   const uint32_t a0 = __builtin_amdgcn_perm(xa, k.L0, 0x0C020400u);
   const uint32_t a1 = __builtin_amdgcn_perm(xa, k.L0, 0x0C020500u);
