@@ -645,11 +645,11 @@ int annety_lhc_parse(const void* h_stream, size_t size, int length_type, int64_t
       rc = 1;  // decode returns -1: invalid length
       break;
     }
-    if (length - 4 > 0xFFFFFFFFll) {  // valid for the codec, but beyond this API's 32-bit lengths
+    if (size - pos - T < (uint64_t)length) break;  // incomplete frame (decode returns 0)
+    if (length - 4 > 0xFFFFFFFFll) {  // a complete frame valid for the codec, beyond this API's 32-bit lengths
       rc = ANNETY_CRC_EINVAL;
       break;
     }
-    if (size - pos - T < (uint64_t)length) break;  // incomplete frame
     payload_off[k] = pos + T;
     payload_len[k] = (uint32_t)(length - 4);
     k++;

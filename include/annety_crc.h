@@ -95,8 +95,8 @@ int annety_crc32_batch_fixed_host(const void* h_base, size_t n, size_t len, size
  * stopping at the first incomplete frame, at max_frames, or at an invalid length (length < 4, or
  * length > max_payload when max_payload > 0, or a negative signed length as peek_int* would read it).
  * *n_frames = frames written, *consumed = bytes of those frames. Returns 0; 1 when it stopped on an
- * invalid length at offset *consumed (decode's -1); ANNETY_CRC_EINVAL for a bad argument or a frame
- * whose payload is 4 GiB or more (lengths here are 32-bit). */
+ * invalid length at offset *consumed (decode's -1); ANNETY_CRC_EINVAL for a bad argument or a complete
+ * frame whose payload is 4 GiB or more (lengths here are 32-bit). */
 int annety_lhc_parse(const void* h_stream, size_t size, int length_type, int64_t max_payload, uint64_t* payload_off,
                      uint32_t* payload_len, size_t max_frames, size_t* n_frames, size_t* consumed);
 /* Device verify of n frames already located (offsets/lengths from annety_lhc_parse, copied to the

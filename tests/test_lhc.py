@@ -302,3 +302,57 @@ def test_cpp_batch_codec_host_side(golden, tmp_path):
                 want.append(f"{r}:{pos}")
                 pos += T + n + 4 if r == 1 else 0
             assert plan[1:] == want and int(plan[0]) == pos
+
+
+# ---------------- property tests of the host walk (hypothesis) ----------------
+from hypothesis import given, settings, strategies as st  # noqa: E402
+
+
+@st.composite
+def _streams(draw):
+    T = draw(st.sampled_from([1, 2, 4, 8]))
+    maxp = draw(st.sampled_from([0, -1, 40, 1 << 26]))
+    parts = []
+    for i in range(draw(st.integers(0, 12))):
+        kind = draw(st.sampled_from(["frame", "frame", "frame", "flip", "junk"]))
+        if kind == "junk":
+            parts.append(draw(st.binary(min_size=1, max_size=12)))
+            continue
+        n = draw(st.integers(1, 100 if T == 1 else 300))
+        _, f = oracle.lhc_encode(_payload(n, 31 * i + n), T, 0)
+        if kind == "flip" and len(f) > T:
+            b = bytearray(f)
+            b[draw(st.integers(T, len(f) - 1))] ^= 1 << draw(st.integers(0, 7))
+            f = bytes(b)
+        parts.append(f)
+    s = b"".join(parts)
+    cut = draw(st.integers(0, len(s)))
+    return T, maxp, s[:cut]
+
+
+@settings(max_examples=300, deadline=None)
+@given(_streams())
+def test_property_walk_and_recv_equal_reference_semantics(case):
+    """On arbitrary streams (valid frames, bit flips anywhere including headers, junk, truncation), the
+    host walk + per-frame verdicts give exactly the oracle's Codec::recv sequence."""
+    T, maxp, s = case
+    codec = LengthHeaderCodec(T, True, maxp)
+    off, ln, used, invalid = codec.parse(s)
+    r = recv_result(T, off, ln, used, invalid, _cpu_verdicts(s, off, ln))
+    frames, consumed, rt = oracle.lhc_recv(s, T, maxp)
+    assert [(int(o), int(n)) for o, n in zip(r.payload_off, r.payload_len)] == frames
+    assert (r.consumed, r.rt) == (consumed, rt)
+
+
+@settings(max_examples=200, deadline=None)
+@given(st.lists(st.integers(0, 5000), max_size=40), st.sampled_from([1, 2, 4, 8]),
+       st.sampled_from([0, -1, 100, 4096]))
+def test_property_plan_equals_sequential_encode(lens, T, maxp):
+    """encode_plan = what consecutive LengthHeaderCodec::encode calls append to one buffer."""
+    off, rt, total = LengthHeaderCodec(T, True, maxp).plan(np.array(lens, dtype=np.uint32))
+    pos = 0
+    for i, n in enumerate(lens):
+        r, out = oracle.lhc_encode(_payload(n, i), T, maxp)
+        assert int(rt[i]) == r and int(off[i]) == pos
+        pos += len(out)
+    assert total == pos
