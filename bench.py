@@ -47,6 +47,24 @@ def parse():
     return p.parse_args()
 
 
+def zipf_batch(seed: int, target: int = 1 << 30):
+    """k ~ Zipf(1.1) over ranks 1..1024, L = min(65536, 64k + r), r ~ U{0..63},
+    packed back-to-back (unaligned starts), sum just under `target` bytes. Returns (lengths, offsets) int64."""
+    rng = np.random.default_rng(seed)
+    p = np.arange(1, 1025, dtype=np.float64) ** -1.1
+    p /= p.sum()
+    lens, total = [], 0
+    while total < target:
+        k = rng.choice(1024, size=65536, p=p) + 1
+        ln = np.minimum(65536, 64 * k + rng.integers(0, 64, 65536))
+        lens.append(ln)
+        total += int(ln.sum())
+    lens = np.concatenate(lens)
+    lens = lens[: int(np.searchsorted(np.cumsum(lens), target))].astype(np.int64)
+    offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    return lens, offs
+
+
 class Workload:
     """One batch resident on the device plus everything the report needs about it."""
 
@@ -71,20 +89,7 @@ class Workload:
             self.desc = (f"BASELINE config {args.config}: {n} x {L} B payloads contiguous in HBM per GPU, "
                          "one batch launch per step")
         else:
-            # k ~ Zipf(1.1) over ranks 1..1024, L = min(65536, 64k + r), r ~ U{0..63},
-            # packed back-to-back (unaligned starts), sum ~ 1 GiB.
-            rng = np.random.default_rng(0x5EED + rank)
-            p = np.arange(1, 1025, dtype=np.float64) ** -1.1
-            p /= p.sum()
-            lens, total = [], 0
-            while total < (1 << 30):
-                k = rng.choice(1024, size=65536, p=p) + 1
-                ln = np.minimum(65536, 64 * k + rng.integers(0, 64, 65536))
-                lens.append(ln)
-                total += int(ln.sum())
-            lens = np.concatenate(lens)
-            lens = lens[: int(np.searchsorted(np.cumsum(lens), 1 << 30))].astype(np.int64)
-            offs = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+            lens, offs = zipf_batch(0x5EED + rank)
             total = int(lens.sum())
             self.n, self.L = len(lens), None
             self.data = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=gen)

@@ -13,14 +13,26 @@
 
 using namespace annety_crc;
 
+// Every stage is synchronised and checked (stage name on stdout, line-buffered) so a failure names
+// the stage that caused it.
+#define STAGE(name)                                                                        \
+  do {                                                                                     \
+    hipError_t e_ = hipDeviceSynchronize();                                                \
+    if (e_ == hipSuccess) e_ = hipGetLastError();                                          \
+    printf("stage %-28s %s\n", name, e_ == hipSuccess ? "ok" : hipGetErrorString(e_));     \
+    if (e_ != hipSuccess) exit(2);                                                         \
+  } while (0)
+#define RC(x) do { int r_ = (x); if (r_) { printf("%s -> %d (%s)\n", #x, r_, annety_crc_strerror(r_)); exit(3); } } while (0)
+
 template <int G, int PROBE>
 void launch_cls(DeviceCtx& c, const void* base, size_t n, const void* desc, const uint32_t* range, uint32_t* out) {
-  hipLaunchKernelGGL((crc32_var_kernel<G, true, false, kVwg, PROBE>), dim3(256), dim3(kBlock), 0, 0,
+  hipLaunchKernelGGL((crc32_var_kernel<G, true, false, kVwg, PROBE>), dim3(c.cus), dim3(kBlock), 0, 0,
                      (const uint8_t*)base, n, (uint64_t)0, 0u, (const uint4*)desc, range, (const uint4*)c.d_slice,
                      (const uint4*)group_image(c, G), (const uint4*)c.d_unshift, c.d_short, out);
 }
 
 int main() {
+  setvbuf(stdout, nullptr, _IOLBF, 0);
   // SURVEY.md §8d config 3 lengths
   std::mt19937_64 rng(0x5EED);
   std::vector<double> cdf(1024);
@@ -47,12 +59,16 @@ int main() {
   CK(hipMemcpy(doff, offs.data(), n * 8, hipMemcpyHostToDevice));
   CK(hipMemcpy(dlen, lens.data(), n * 4, hipMemcpyHostToDevice));
   DeviceCtx* c = nullptr;
-  if (annety_crc_init(0) || current_ctx(&c)) return 1;
+  RC(annety_crc_init(0));
+  RC(current_ctx(&c));
+  STAGE("setup");
   // clocks up: fixed batches inside the arena (total + 256 bytes allocated)
   uint32_t* warm;
   CK(hipMalloc(&warm, (total / 1024) * 4));
-  for (int r = 0; r < 3000; r++) annety_crc32_batch_fixed(d, total / 1024, 1024, 1024, warm, nullptr);
-  if (annety_crc32_batch_var(d, doff, dlen, n, ref, nullptr)) return 1;
+  for (int r = 0; r < 3000; r++) RC(annety_crc32_batch_fixed(d, total / 1024, 1024, 1024, warm, nullptr));
+  STAGE("warm fixed batches");
+  RC(annety_crc32_batch_var(d, doff, dlen, n, ref, nullptr));
+  STAGE("reference batch_var");
   const size_t rows_words = (size_t)bucket_blocks(n) * bucket_count();
   uint32_t *rows, *ranges; void* desc;
   CK(hipMalloc(&rows, rows_words * 4)); CK(hipMalloc(&ranges, 64)); CK(hipMalloc(&desc, 16 * n));
@@ -62,6 +78,7 @@ int main() {
     CK(hipEventRecord(e0));
     for (int r = 0; r < 30; r++) launch();
     CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1));
+    STAGE(name);
     float ms; CK(hipEventElapsedTime(&ms, e0, e1));
     bool ok = true;
     if (check) {
@@ -73,7 +90,7 @@ int main() {
     printf("%-40s %.4f ms  %.1f GB/s %s\n", name, ms / 30, total / (ms / 30) / 1e6, check ? (ok ? "ok" : "MISMATCH") : "");
   };
   auto bucket = [&] { CK(launch_bucket(d, n, doff, dlen, rows, ranges, desc, out, nullptr)); };
-  b2b([&] { annety_crc32_batch_var(d, doff, dlen, n, out, nullptr); }, "product batch_var", true);
+  b2b([&] { RC(annety_crc32_batch_var(d, doff, dlen, n, out, nullptr)); }, "product batch_var", true);
   b2b(bucket, "bucket passes only", false);
   bucket();
   CK(hipDeviceSynchronize());

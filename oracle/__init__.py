@@ -58,6 +58,9 @@ def _load_oracle() -> ctypes.CDLL:
     lib.oracle_crc32_batch_fixed_mt.restype = ctypes.c_int
     lib.oracle_crc32_batch_fixed_mt.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
                                                 ctypes.c_void_p, ctypes.c_int]
+    lib.oracle_crc32_batch_var_mt.restype = ctypes.c_int
+    lib.oracle_crc32_batch_var_mt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                              ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
     lib.oracle_lcg_fill.restype = ctypes.c_uint64
     lib.oracle_lcg_fill.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint64]
     lib.oracle_tables.restype = None
@@ -145,6 +148,27 @@ def batch_var(buf: np.ndarray, offsets: np.ndarray, lengths: np.ndarray) -> np.n
         raise ValueError("batch exceeds buffer")
     out = np.zeros(off.size, dtype=np.uint32)
     _lib.oracle_crc32_batch_var(_ptr(a), _ptr(off), _ptr(ln), off.size, _ptr(out))
+    return out
+
+
+def batch_var_mt(buf: np.ndarray, offsets: np.ndarray, lengths: np.ndarray, threads: int = 1,
+                 states: np.ndarray | None = None) -> np.ndarray:
+    """Variable batch over `threads` host threads: crc32_long per payload, or (states given)
+    crc32_update of each payload from its register (returns the new registers)."""
+    a = _as_u8(buf)
+    off = np.ascontiguousarray(offsets, dtype=np.uint64)
+    ln = np.ascontiguousarray(lengths, dtype=np.uint32)
+    if off.size and int((off + ln.astype(np.uint64)).max()) > a.size:
+        raise ValueError("batch exceeds buffer")
+    if states is None:
+        out = np.zeros(off.size, dtype=np.uint32)
+    else:
+        out = np.array(states, dtype=np.uint32, copy=True)
+        if out.size != off.size:
+            raise ValueError("one register per payload")
+    if _lib.oracle_crc32_batch_var_mt(_ptr(a), _ptr(off), _ptr(ln), off.size, _ptr(out), int(states is not None),
+                                      threads) != 0:
+        raise RuntimeError("pthread_create failed")
     return out
 
 

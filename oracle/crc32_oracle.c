@@ -216,3 +216,43 @@ int oracle_lhc_decode(int T, int64_t max_payload, const unsigned char* s, size_t
   *consumed = (size_t)T + (size_t)length;
   return 1;
 }
+
+/* Variable batches over T threads (payload-parallel, as above): digests (crc32_long) or, with
+ * `update` set, crc32_update of out[i] in place (include/Crc32c.h:71-82). Test checker for the
+ * full-size variable-length parity cases (BASELINE config 3) and the cpu_baseline leg. */
+typedef struct {
+  const unsigned char* base;
+  const uint64_t* off;
+  const uint32_t* len;
+  size_t lo, hi;
+  uint32_t* out;
+  int update;
+} vjob_t;
+static void* vworker(void* p) {
+  vjob_t* j = (vjob_t*)p;
+  for (size_t i = j->lo; i < j->hi; i++) {
+    if (j->update)
+      oracle_crc32_update(&j->out[i], j->base + j->off[i], j->len[i]);
+    else
+      j->out[i] = oracle_crc32_long(j->base + j->off[i], j->len[i]);
+  }
+  return NULL;
+}
+int oracle_crc32_batch_var_mt(const unsigned char* base, const uint64_t* off, const uint32_t* len, size_t n,
+                              uint32_t* out, int update, int threads) {
+  ensure();
+  if (threads < 1) threads = 1;
+  if (threads > 256) threads = 256;
+  pthread_t tid[256];
+  vjob_t jobs[256];
+  for (int t = 0; t < threads; t++) {
+    vjob_t j = {base, off, len, n * (size_t)t / threads, n * (size_t)(t + 1) / threads, out, update};
+    jobs[t] = j;
+    if (pthread_create(&tid[t], NULL, vworker, &jobs[t]) != 0) {
+      for (int k = 0; k < t; k++) pthread_join(tid[k], NULL);
+      return -1;
+    }
+  }
+  for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
+  return 0;
+}

@@ -1,0 +1,83 @@
+"""Full-size parity at the BASELINE shapes the bench runs (configs 2 and 3), through the C-ABI.
+
+Config 3: the bench's own Zipf batch (~164k payloads, 1 GiB, packed back-to-back so starts are
+unaligned), digests AND crc32_update registers compared bit-exactly with the multi-threaded oracle
+on every payload. Config 2: 4096 x 4 MiB = 16 GiB resident, compared on every payload.
+Each test prints its progress so a stall names its stage.
+"""
+import os
+import sys
+
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+THREADS = 16  # the GPU box's CPU share for one GPU
+
+
+def _bench():
+    if ROOT not in sys.path:
+        sys.path.insert(0, ROOT)
+    import bench
+
+    return bench
+
+
+def _u32(t):
+    import torch
+
+    torch.cuda.synchronize()
+    return t.cpu().numpy().view(np.uint32)
+
+
+def test_config3_full_bitexact(gpu):
+    import torch
+
+    import annety_amd
+
+    lens, offs = _bench().zipf_batch(0x5EED)
+    total = int(lens.sum())
+    g = torch.Generator(device=gpu)
+    g.manual_seed(31337)
+    data = torch.randint(0, 256, (total,), dtype=torch.uint8, device=gpu, generator=g)
+    d_off = torch.from_numpy(offs).to(gpu)
+    d_len = torch.from_numpy(lens.astype(np.int32)).to(gpu)
+    print(f"config 3: {lens.size} payloads, {total / 2**30:.3f} GiB", flush=True)
+    got = _u32(annety_amd.crc32_batch_var(data, d_off, d_len))
+    print("config 3: digests done", flush=True)
+    host = data.cpu().numpy()
+    want = oracle.batch_var_mt(host, offs, lens, THREADS)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"{bad.size} digest mismatches, first {bad[:8]} (lengths {lens[bad[:8]]})"
+
+    rng = np.random.default_rng(3)
+    states = rng.integers(0, 2 ** 32, lens.size, dtype=np.uint64).astype(np.uint32)
+    d_state = torch.from_numpy(states.view(np.int32).copy()).to(gpu)
+    annety_amd.crc32_update_batch_var(d_state, data, d_off, d_len)
+    got = _u32(d_state)
+    print("config 3: update registers done", flush=True)
+    want = oracle.batch_var_mt(host, offs, lens, THREADS, states=states)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"{bad.size} register mismatches, first {bad[:8]}"
+
+
+def test_config2_full_bitexact(gpu):
+    import torch
+
+    import annety_amd
+
+    n, L = 4096, 4 << 20
+    g = torch.Generator(device=gpu)
+    g.manual_seed(2222)
+    data = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=gpu, generator=g)
+    print("config 2: 16 GiB resident", flush=True)
+    got = _u32(annety_amd.crc32_batch(data, n, L))
+    host = data.cpu().numpy()
+    del data
+    torch.cuda.empty_cache()
+    want = oracle.batch_fixed_mt(host, n, L, threads=THREADS)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"{bad.size} mismatches, first {bad[:8]}"
