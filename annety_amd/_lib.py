@@ -31,10 +31,13 @@ SIGNATURES = [
     ("annety_crc32_batch_var", ctypes.c_int, [_vp, _vp, _vp, _c_size, _vp, _vp]),
     ("annety_crc32_update_batch_fixed", ctypes.c_int, [_vp, _vp, _c_size, _c_size, _c_size, _vp]),
     ("annety_crc32_update_batch_var", ctypes.c_int, [_vp, _vp, _vp, _vp, _c_size, _vp]),
+    ("annety_crc32_batch_var_arena", ctypes.c_int, [_vp, _c_size, _vp, _vp, _c_size, _vp, _vp]),
+    ("annety_crc32_update_batch_var_arena", ctypes.c_int, [_vp, _vp, _c_size, _vp, _vp, _c_size, _vp]),
     ("annety_crc32_batch_fixed_host", ctypes.c_int, [_vp, _c_size, _c_size, _c_size, _vp]),
     ("annety_lhc_parse", ctypes.c_int, [_vp, _c_size, ctypes.c_int, ctypes.c_int64, _vp, _vp, _c_size,
                                         ctypes.POINTER(_c_size), ctypes.POINTER(_c_size)]),
     ("annety_lhc_verify_batch", ctypes.c_int, [_vp, _vp, _vp, _c_size, _vp, _vp, _vp]),
+    ("annety_lhc_verify_stream", ctypes.c_int, [_vp, _c_size, _vp, _vp, _c_size, _vp, _vp, _vp]),
     ("annety_lhc_encode_plan", ctypes.c_int, [_vp, _c_size, ctypes.c_int, ctypes.c_int64, _vp, _vp,
                                               ctypes.POINTER(_u64)]),
     ("annety_lhc_encode_batch", ctypes.c_int, [_vp, _vp, _vp, _c_size, ctypes.c_int, ctypes.c_int64, _vp, _vp,

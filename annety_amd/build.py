@@ -14,8 +14,8 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(ROOT, "include")
 LIB = os.path.join(PKG, "libannety_crc.so")
-SOURCES = ["crc32_kernels.hip", "crc32_frames.hip", "crc32_capi.cpp"]
-HEADERS = ["crc32_kernels.h", "crc32_math.h"]
+SOURCES = ["crc32_kernels.hip", "crc32_arena.hip", "crc32_frames.hip", "crc32_capi.cpp"]
+HEADERS = ["crc32_kernels.h", "crc32_math.h", "crc32_device.h"]
 ARCH = "gfx950"
 
 

@@ -23,7 +23,7 @@ from dataclasses import dataclass
 import numpy as np
 
 from . import _lib
-from .crc32c import BytesLike, _dev_ptr, _host_view, _require_device, _stream_handle
+from .crc32c import BytesLike, _dev_ptr, _host_view, _on_device, _require_device, _stream_handle
 
 DEFAULT_MAX_PAYLOAD = 64 * 1024 * 1024  # LengthHeaderCodec ctor default (:50)
 
@@ -99,18 +99,27 @@ class LengthHeaderCodec:
             _lib.check(st, "annety_lhc_parse")
         return off[: k.value], ln[: k.value], int(used.value), st == 1
 
-    def verify(self, d_stream, d_off, d_len, out_ok=None, out_digest=None, stream=None):
-        """Device checksum check of located frames: ok uint8[n] (1 = trailer matches)."""
+    def verify(self, d_stream, d_off, d_len, out_ok=None, out_digest=None, stream=None, arena=True):
+        """Device checksum check of located frames: ok uint8[n] (1 = trailer matches).
+        arena=True (default): the frames fill d_stream, one pass over the stream (annety_lhc_verify_stream);
+        False: the general variable-length path (annety_lhc_verify_batch)."""
         import torch
 
         _require_device(d_stream, "d_stream")
         n = int(d_off.numel())
         if out_ok is None:
             out_ok = torch.empty(n, dtype=torch.uint8, device=d_stream.device)
-        st = _lib.get().annety_lhc_verify_batch(_dev_ptr(d_stream), _dev_ptr(d_off), _dev_ptr(d_len), n,
-                                                _dev_ptr(out_ok), _dev_ptr(out_digest) if out_digest is not None
-                                                else None, _stream_handle(stream, out_ok))
-        _lib.check(st, "annety_lhc_verify_batch")
+        dig = _dev_ptr(out_digest) if out_digest is not None else None
+        with _on_device(d_stream, d_off, d_len, out_ok):
+            sh = _stream_handle(stream, out_ok)
+            if arena:
+                nbytes = int(d_stream.numel() * d_stream.element_size())
+                st = _lib.get().annety_lhc_verify_stream(_dev_ptr(d_stream), nbytes, _dev_ptr(d_off), _dev_ptr(d_len),
+                                                         n, _dev_ptr(out_ok), dig, sh)
+            else:
+                st = _lib.get().annety_lhc_verify_batch(_dev_ptr(d_stream), _dev_ptr(d_off), _dev_ptr(d_len), n,
+                                                        _dev_ptr(out_ok), dig, sh)
+        _lib.check(st, "annety_lhc_verify_" + ("stream" if arena else "batch"))
         return out_ok
 
     def decode_batch(self, stream: BytesLike, d_stream=None, device=None) -> DecodeResult:
@@ -164,8 +173,9 @@ class LengthHeaderCodec:
             d_soff = torch.from_numpy(src_off.view(np.int64)).to(dev)
             d_len = torch.from_numpy(lengths.view(np.int32)).to(dev)
             d_foff = torch.from_numpy(frame_off.view(np.int64)).to(dev)
-            st = _lib.get().annety_lhc_encode_batch(_dev_ptr(d_src), _dev_ptr(d_soff), _dev_ptr(d_len), n,
-                                                    self.length_type, self.max_payload, _dev_ptr(frames),
-                                                    _dev_ptr(d_foff), _stream_handle(stream, frames))
+            with _on_device(d_src, frames):
+                st = _lib.get().annety_lhc_encode_batch(_dev_ptr(d_src), _dev_ptr(d_soff), _dev_ptr(d_len), n,
+                                                        self.length_type, self.max_payload, _dev_ptr(frames),
+                                                        _dev_ptr(d_foff), _stream_handle(stream, frames))
             _lib.check(st, "annety_lhc_encode_batch")
         return EncodeResult(frames, frame_off, rt)

@@ -106,6 +106,30 @@ def _require_device(t, name: str) -> None:
         raise ValueError(f"{name} must be a device (ROCm) tensor; the batch path has no CPU fallback")
 
 
+def _on_device(*tensors):
+    """Context making the tensors' device current for the C call: the C-ABI picks its per-device state
+    (LDS table images, scratch pool) from hipGetDevice(), so it must match where the data lives."""
+    import contextlib
+
+    import torch
+
+    devs = {t.device for t in tensors if hasattr(t, "device")}
+    if len(devs) > 1:
+        raise ValueError(f"batch tensors are on different devices: {sorted(str(d) for d in devs)}")
+    return torch.cuda.device(devs.pop()) if devs else contextlib.nullcontext()
+
+
+def _arena_bytes(data, arena) -> Optional[int]:
+    """None: general (sparse) path; True: the whole of `data`; int: that many bytes from data[0]."""
+    if arena is None or arena is False:
+        return None
+    if arena is True:
+        if not hasattr(data, "numel"):
+            raise ValueError("arena=True needs a tensor; pass the arena size in bytes for a raw pointer")
+        return int(data.numel() * data.element_size())
+    return int(arena)
+
+
 def crc32_batch(data, n: int, length: int, stride: Optional[int] = None, out=None, stream=None):
     """Digests of n fixed-length payloads: payload i = data[i*stride : i*stride + length].
 
@@ -121,15 +145,18 @@ def crc32_batch(data, n: int, length: int, stride: Optional[int] = None, out=Non
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=data.device)
     _require_device(out, "out")
-    st = _lib.get().annety_crc32_batch_fixed(_dev_ptr(data), n, length, stride, _dev_ptr(out),
-                                             _stream_handle(stream, out))
+    with _on_device(data, out):
+        st = _lib.get().annety_crc32_batch_fixed(_dev_ptr(data), n, length, stride, _dev_ptr(out),
+                                                 _stream_handle(stream, out))
     _lib.check(st, "annety_crc32_batch_fixed")
     return out
 
 
-def crc32_batch_var(data, offsets, lengths, out=None, stream=None):
+def crc32_batch_var(data, offsets, lengths, out=None, stream=None, arena=None):
     """Digests of payload i = data[offsets[i] : offsets[i] + lengths[i]] (any alignment).
-    offsets: int64 device tensor, lengths: int32 device tensor."""
+    offsets: int64 device tensor, lengths: int32 device tensor.
+    arena: None = general path (length-bucketed, any layout); True / a byte count = the payloads lie in
+    data[0 : arena] and cover most of it (packed batch, frame stream): one pass over the arena."""
     import torch
 
     _require_device(data, "data")
@@ -138,9 +165,16 @@ def crc32_batch_var(data, offsets, lengths, out=None, stream=None):
         raise ValueError("offsets must be int64[n] and lengths int32[n]")
     if out is None:
         out = torch.empty(n, dtype=torch.int32, device=data.device)
-    st = _lib.get().annety_crc32_batch_var(_dev_ptr(data), _dev_ptr(offsets), _dev_ptr(lengths), n, _dev_ptr(out),
-                                           _stream_handle(stream, out))
-    _lib.check(st, "annety_crc32_batch_var")
+    ab = _arena_bytes(data, arena)
+    with _on_device(data, offsets, lengths, out):
+        sh = _stream_handle(stream, out)
+        if ab is None:
+            st = _lib.get().annety_crc32_batch_var(_dev_ptr(data), _dev_ptr(offsets), _dev_ptr(lengths), n,
+                                                   _dev_ptr(out), sh)
+        else:
+            st = _lib.get().annety_crc32_batch_var_arena(_dev_ptr(data), ab, _dev_ptr(offsets), _dev_ptr(lengths), n,
+                                                         _dev_ptr(out), sh)
+    _lib.check(st, "annety_crc32_batch_var" + ("" if ab is None else "_arena"))
     return out
 
 
@@ -149,15 +183,17 @@ def crc32_update_batch(state, data, n: int, length: int, stride: Optional[int] =
     stride = length if stride is None else stride
     _require_device(data, "data")
     _require_device(state, "state")
-    st = _lib.get().annety_crc32_update_batch_fixed(_dev_ptr(state), _dev_ptr(data), n, length, stride,
-                                                    _stream_handle(stream, state))
+    with _on_device(data, state):
+        st = _lib.get().annety_crc32_update_batch_fixed(_dev_ptr(state), _dev_ptr(data), n, length, stride,
+                                                        _stream_handle(stream, state))
     _lib.check(st, "annety_crc32_update_batch_fixed")
     return state
 
 
-def crc32_update_batch_var(state, data, offsets, lengths, stream=None):
+def crc32_update_batch_var(state, data, offsets, lengths, stream=None, arena=None):
     """Streaming update: state[i] (int32 device tensor, uint32 bit patterns) advanced in place over
-    fragment i = data[offsets[i] : offsets[i] + lengths[i]] (crc32_update semantics)."""
+    fragment i = data[offsets[i] : offsets[i] + lengths[i]] (crc32_update semantics). `arena` as in
+    crc32_batch_var."""
     import torch
 
     _require_device(data, "data")
@@ -165,9 +201,16 @@ def crc32_update_batch_var(state, data, offsets, lengths, stream=None):
     n = int(offsets.numel())
     if offsets.dtype != torch.int64 or lengths.dtype != torch.int32 or lengths.numel() != n or state.numel() != n:
         raise ValueError("offsets must be int64[n], lengths int32[n], state int32[n]")
-    st = _lib.get().annety_crc32_update_batch_var(_dev_ptr(state), _dev_ptr(data), _dev_ptr(offsets),
-                                                  _dev_ptr(lengths), n, _stream_handle(stream, state))
-    _lib.check(st, "annety_crc32_update_batch_var")
+    ab = _arena_bytes(data, arena)
+    with _on_device(data, offsets, lengths, state):
+        sh = _stream_handle(stream, state)
+        if ab is None:
+            st = _lib.get().annety_crc32_update_batch_var(_dev_ptr(state), _dev_ptr(data), _dev_ptr(offsets),
+                                                          _dev_ptr(lengths), n, sh)
+        else:
+            st = _lib.get().annety_crc32_update_batch_var_arena(_dev_ptr(state), _dev_ptr(data), ab,
+                                                                _dev_ptr(offsets), _dev_ptr(lengths), n, sh)
+    _lib.check(st, "annety_crc32_update_batch_var" + ("" if ab is None else "_arena"))
     return state
 
 
@@ -182,8 +225,8 @@ class StreamingCrc:
 
         self.state = torch.full((n_streams,), -1, dtype=torch.int32, device=device or "cuda")
 
-    def update(self, data, offsets, lengths, stream=None):
-        crc32_update_batch_var(self.state, data, offsets, lengths, stream)
+    def update(self, data, offsets, lengths, stream=None, arena=None):
+        crc32_update_batch_var(self.state, data, offsets, lengths, stream, arena)
         return self
 
     def digests(self):

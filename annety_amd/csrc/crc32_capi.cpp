@@ -46,6 +46,8 @@ struct HostImages {
   std::vector<uint32_t> slice;   // common part: slicing tables (32768 words) + half-line join (128 words)
   std::vector<uint32_t> groups;  // kNumGroups * (kGroupImageBytes / 4)
   std::vector<uint32_t> unshift; // 24 maps x 128 words (U_lo[0..15], U_hi[0..7])
+  std::vector<uint32_t> sb;      // arena superblock join: (k, v, g) = shift_{(7-g)*1024}(v << 4k)
+  std::vector<uint32_t> stitch;  // arena stitch: level maps shift_{128*8^L} (3 x 128 words) + unshift
   uint32_t short_init[4];
 };
 
@@ -128,6 +130,16 @@ const HostImages& host_images() {
       acc = gf2_mul(inv16, acc);
     }
     for (int l = 0; l < 4; l++) img.short_init[l] = shift_bits(kInit, 8u * l);
+    img.sb.assign(kLdsSbJoinBytes / 4, 0);
+    for (uint32_t g = 0; g < 8; g++) {
+      uint32_t nt[8 * 16];
+      nibble_tables(shift_matrix((uint64_t)(7 - g) * 1024), nt);
+      for (int kk = 0; kk < 8; kk++)
+        for (int v = 0; v < 16; v++) img.sb[kk * 128 + v * 8 + g] = nt[kk * 16 + v];
+    }
+    img.stitch.assign((kLdsStitchImageBytes - kLdsCommonBytes) / 4, 0);
+    for (int L = 0; L < 3; L++) nibble_tables(shift_matrix((uint64_t)128 << (3 * L)), img.stitch.data() + L * 128);
+    std::memcpy(img.stitch.data() + kLdsLevelBytes / 4, img.unshift.data(), img.unshift.size() * 4);
   });
   return img;
 }
@@ -150,6 +162,9 @@ struct DeviceCtx {
   void* d_groups = nullptr;
   uint32_t* d_unshift = nullptr;
   uint32_t* d_short = nullptr;
+  void* d_sb = nullptr;
+  void* d_stitch = nullptr;
+  void* d_zero = nullptr;  // 256 zero bytes
   Staging stg;
   std::mutex stg_mu;  // one host-staged batch at a time per device
   std::mutex pow_mu;  // split-path power tables, one per segment size
@@ -180,6 +195,12 @@ int init_device_locked(int dev) {
     if ((e = hipMalloc(&c.d_groups, img.groups.size() * 4)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMalloc(&c.d_unshift, img.unshift.size() * 4)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMalloc(&c.d_short, 16)) != hipSuccess) { rc = hip_fail(e); break; }
+    if ((e = hipMalloc(&c.d_sb, img.sb.size() * 4)) != hipSuccess) { rc = hip_fail(e); break; }
+    if ((e = hipMalloc(&c.d_stitch, img.stitch.size() * 4)) != hipSuccess) { rc = hip_fail(e); break; }
+    if ((e = hipMalloc(&c.d_zero, 256)) != hipSuccess) { rc = hip_fail(e); break; }
+    if ((e = hipMemset(c.d_zero, 0, 256)) != hipSuccess) { rc = hip_fail(e); break; }
+    if ((e = hipMemcpy(c.d_sb, img.sb.data(), img.sb.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_fail(e); break; }
+    if ((e = hipMemcpy(c.d_stitch, img.stitch.data(), img.stitch.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMemcpy(c.d_slice, img.slice.data(), img.slice.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMemcpy(c.d_groups, img.groups.data(), img.groups.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMemcpy(c.d_unshift, img.unshift.data(), img.unshift.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_fail(e); break; }
@@ -284,6 +305,51 @@ int run_var_sorted(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d
     rc = run_var(c, d_base, n, 0, 0, groups[k], desc, ranges + 2 * k, d_out, stream, update);
   e = hipFreeAsync(scratch, stream);
   if (rc == ANNETY_CRC_OK && e != hipSuccess) rc = hip_fail(e);
+  return rc;
+}
+
+// Arena path (crc32_arena.hip): one bulk pass over every line of [d_base, d_base + arena_bytes),
+// then one lane per payload. Scratch (c1, c8, c64: 73 words per 8 KiB superblock, ~3.6 % of the
+// arena) comes from the stream-ordered allocator.
+int run_arena(DeviceCtx& c, const void* d_base, size_t arena_bytes, const uint64_t* d_off, const uint32_t* d_len,
+              size_t n, uint32_t* d_out, hipStream_t stream, bool update) {
+  ArenaLaunch a{};
+  a.base = d_base;
+  a.off = d_off;
+  a.len = d_len;
+  a.n = n;
+  a.out = d_out;
+  a.update = update;
+  a.img_slice = c.d_slice;
+  a.img_group8 = group_image(c, 8);
+  a.img_sb = c.d_sb;
+  a.img_stitch = c.d_stitch;
+  a.zero_line = c.d_zero;
+  a.max_blocks = (size_t)c.cus;
+  a.line_lo = 1;  // empty arena: every payload folds its lines directly
+  a.line_hi = 0;
+  uint32_t* scratch = nullptr;
+  if (arena_bytes) {
+    const uint64_t a0 = (uint64_t)(uintptr_t)d_base;
+    a.line_lo = a0 >> 7;
+    a.line_hi = (a0 + arena_bytes - 1) >> 7;
+    a.sb0 = a.line_lo >> 6;
+    a.nsb = (a.line_hi >> 6) - a.sb0 + 1;
+    a.fs0 = (a.line_lo + 63) >> 6;
+    a.fs1 = (a.line_hi + 1) >> 6;
+    if (a.fs1 < a.fs0) a.fs1 = a.fs0;
+    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&scratch), a.nsb * 73 * sizeof(uint32_t), stream));
+    a.c1 = scratch;
+    a.c8 = scratch + a.nsb * 64;
+    a.c64 = a.c8 + a.nsb * 8;
+  }
+  int rc = ANNETY_CRC_OK;
+  hipError_t e = launch_arena(a, stream);
+  if (e != hipSuccess) rc = hip_fail(e);
+  if (scratch) {
+    e = hipFreeAsync(scratch, stream);
+    if (rc == ANNETY_CRC_OK && e != hipSuccess) rc = hip_fail(e);
+  }
   return rc;
 }
 
@@ -422,6 +488,9 @@ int annety_crc_shutdown(void) {
     (void)hipFree(c.d_groups);
     (void)hipFree(c.d_unshift);
     (void)hipFree(c.d_short);
+    (void)hipFree(c.d_sb);
+    (void)hipFree(c.d_stitch);
+    (void)hipFree(c.d_zero);
     for (int i = 0; i < 2; i++) {
       if (c.stg.stream[i]) (void)hipStreamDestroy(c.stg.stream[i]);
       if (c.stg.done[i]) (void)hipEventDestroy(c.stg.done[i]);
@@ -438,6 +507,7 @@ int annety_crc_shutdown(void) {
     }
     c.d_slice = c.d_groups = nullptr;
     c.d_unshift = c.d_short = nullptr;
+    c.d_sb = c.d_stitch = c.d_zero = nullptr;
     c.ready = false;
   }
   (void)hipSetDevice(prev);
@@ -520,6 +590,26 @@ int annety_crc32_batch_var(const void* d_base, const uint64_t* d_off, const uint
   if (rc) return rc;
   if (n > 0xFFFFFFFFull) return ANNETY_CRC_EINVAL;  // order[] holds 32-bit payload indices
   return run_var_sorted(*c, d_base, n, d_off, d_len, d_out, static_cast<hipStream_t>(stream));
+}
+
+int annety_crc32_batch_var_arena(const void* d_arena, size_t arena_bytes, const uint64_t* d_off,
+                                 const uint32_t* d_len, size_t n, uint32_t* d_out, void* stream) {
+  if (n == 0) return ANNETY_CRC_OK;
+  if (!d_arena || !d_off || !d_len || !d_out) return ANNETY_CRC_EINVAL;
+  DeviceCtx* c = nullptr;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  return run_arena(*c, d_arena, arena_bytes, d_off, d_len, n, d_out, static_cast<hipStream_t>(stream), false);
+}
+
+int annety_crc32_update_batch_var_arena(uint32_t* d_state, const void* d_arena, size_t arena_bytes,
+                                        const uint64_t* d_off, const uint32_t* d_len, size_t n, void* stream) {
+  if (n == 0) return ANNETY_CRC_OK;
+  if (!d_state || !d_arena || !d_off || !d_len) return ANNETY_CRC_EINVAL;
+  DeviceCtx* c = nullptr;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  return run_arena(*c, d_arena, arena_bytes, d_off, d_len, n, d_state, static_cast<hipStream_t>(stream), true);
 }
 
 int annety_crc32_update_batch_fixed(uint32_t* d_state, const void* d_base, size_t n, size_t len, size_t stride,
@@ -660,8 +750,8 @@ int annety_lhc_parse(const void* h_stream, size_t size, int length_type, int64_t
   return rc;
 }
 
-int annety_lhc_verify_batch(const void* d_stream, const uint64_t* d_payload_off, const uint32_t* d_payload_len,
-                            size_t n, uint8_t* d_ok, uint32_t* d_digest, void* stream) {
+static int lhc_verify(const void* d_stream, size_t stream_bytes, bool arena, const uint64_t* d_payload_off,
+                      const uint32_t* d_payload_len, size_t n, uint8_t* d_ok, uint32_t* d_digest, void* stream) {
   if (n == 0) return ANNETY_CRC_OK;
   if (!d_stream || !d_payload_off || !d_payload_len || !d_ok) return ANNETY_CRC_EINVAL;
   DeviceCtx* c = nullptr;
@@ -670,7 +760,8 @@ int annety_lhc_verify_batch(const void* d_stream, const uint64_t* d_payload_off,
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint32_t* dig = d_digest;
   if (!dig) HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&dig), n * sizeof(uint32_t), s));
-  rc = annety_crc32_batch_var(d_stream, d_payload_off, d_payload_len, n, dig, stream);
+  rc = arena ? run_arena(*c, d_stream, stream_bytes, d_payload_off, d_payload_len, n, dig, s, false)
+             : annety_crc32_batch_var(d_stream, d_payload_off, d_payload_len, n, dig, stream);
   if (rc == ANNETY_CRC_OK) {
     hipError_t e = launch_lhc_compare(d_stream, d_payload_off, d_payload_len, n, dig, d_ok, s);
     if (e != hipSuccess) rc = hip_fail(e);
@@ -680,6 +771,17 @@ int annety_lhc_verify_batch(const void* d_stream, const uint64_t* d_payload_off,
     if (rc == ANNETY_CRC_OK && e != hipSuccess) rc = hip_fail(e);
   }
   return rc;
+}
+
+int annety_lhc_verify_batch(const void* d_stream, const uint64_t* d_payload_off, const uint32_t* d_payload_len,
+                            size_t n, uint8_t* d_ok, uint32_t* d_digest, void* stream) {
+  return lhc_verify(d_stream, 0, false, d_payload_off, d_payload_len, n, d_ok, d_digest, stream);
+}
+
+int annety_lhc_verify_stream(const void* d_stream, size_t stream_bytes, const uint64_t* d_payload_off,
+                             const uint32_t* d_payload_len, size_t n, uint8_t* d_ok, uint32_t* d_digest,
+                             void* stream) {
+  return lhc_verify(d_stream, stream_bytes, true, d_payload_off, d_payload_len, n, d_ok, d_digest, stream);
 }
 
 // LengthHeaderCodec::encode's per-payload decision (:169-176): rt 0 for an empty payload, -1 for

@@ -65,6 +65,31 @@ hipError_t launch_split_desc(const void* base, size_t n, uint64_t len, uint64_t 
 hipError_t launch_split_join(const uint32_t* seg_crc, size_t n, uint32_t S, const uint32_t* powers, uint32_t* out,
                              hipStream_t stream);
 
+// Arena path (crc32_arena.hip): bulk line pass over [line_lo, line_hi] (absolute 128-byte lines,
+// superblocks of 64 lines from sb0, nsb of them; nsb = 0 skips the pass), then the per-payload stitch.
+struct ArenaLaunch {
+  const void* base;          // payload offsets are relative to this pointer
+  uint64_t line_lo, line_hi; // arena lines (line_lo > line_hi: no arena, every payload folded directly)
+  uint64_t sb0, nsb;         // superblocks (64 lines) overlapping the arena
+  uint64_t fs0, fs1;         // the full ones: [fs0, fs1), absolute superblock indices
+  const uint64_t* off;       // device, n entries
+  const uint32_t* len;       // device, n entries
+  size_t n;
+  uint32_t *c1, *c8, *c64;   // scratch: nsb*64, nsb*8, nsb words
+  const void* img_slice;     // common image part (slicing tables + half-line join)
+  const void* img_group8;    // G = 8 group part (lane join + round maps)
+  const void* img_sb;        // superblock join, kLdsSbJoinBytes
+  const void* img_stitch;    // level maps + inverse shifts, kLdsStitchImageBytes - kLdsCommonBytes
+  const void* zero_line;     // 128 zero bytes (device), read in place of lines outside the arena
+  uint32_t* out;             // digests, or (update) registers in place
+  size_t max_blocks;
+  bool update;
+};
+
+hipError_t launch_arena(const ArenaLaunch& a, hipStream_t stream);
+// the line pass alone (crc32_kernels.hip: the config-1 kernel in arena mode)
+hipError_t launch_arena_lines(const ArenaLaunch& a, hipStream_t stream);
+
 // LengthHeaderCodec frames (crc32_frames.hip)
 hipError_t launch_lhc_compare(const void* stream_base, const uint64_t* off, const uint32_t* len, size_t n,
                               const uint32_t* digest, uint8_t* ok, hipStream_t stream);

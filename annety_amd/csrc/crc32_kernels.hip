@@ -14,141 +14,12 @@
 
 #include <algorithm>
 
+#include "crc32_device.h"
 #include "crc32_kernels.h"
 #include "crc32_math.h"
 
 namespace annety_crc {
 namespace {
-
-constexpr int kBlock = 512;
-// Threads per virtual workgroup (0 = off): the lane-groups of one 512-thread block are taken from
-// two virtual blocks gridDim.x apart instead of one contiguous run (microbench/mb_crc.hip `mv`:
-// 6.43 vs 6.17 TB/s for the same load/LDS structure).
-constexpr int kVwg = 256;
-
-// Lane-group index of this thread under the virtual-workgroup mapping (a bijection onto
-// [0, gridDim.x * BLK / G) for VWG a multiple of G that divides BLK).
-template <int BLK, int G, int VWG>
-__device__ __forceinline__ size_t group_id() {
-  if constexpr (VWG == 0 || VWG >= BLK) {
-    return (blockIdx.x * (size_t)BLK + threadIdx.x) / G;
-  } else {
-    const size_t v = blockIdx.x + (size_t)gridDim.x * (threadIdx.x / VWG);
-    return (v * VWG + threadIdx.x % VWG) / G;
-  }
-}
-
-__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
-  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);
-}
-
-struct LaneCtx {
-  uint32_t L0;     // (replica*8) in byte 0, pair 0 in byte 2
-  uint32_t L1;     // (replica*8) in byte 0, pair 1 in byte 2
-  uint32_t slot4;  // replica*4 for the 4-byte join tables
-};
-
-// Absorb one 32-bit word per chain, two chains at once. x = register ^ word (little-endian bytes
-// b0..b3) becomes T3[b0]^T2[b1]^T1[b2]^T0[b3] ^ wnext, i.e. the register after the word, pre-xored with
-// the chain's next word. The eight ds_read_b64 are issued back-to-back through inline asm so the
-// compiler cannot narrow them to ds_read_b32 (which would use the 32-bank rule and conflict 2-way);
-// the single wait is tied to the results.
-__device__ __forceinline__ void word4x2(uint32_t& xa, uint32_t wa, uint32_t& xb, uint32_t wb, const LaneCtx& k) {
-  const uint32_t a0 = __builtin_amdgcn_perm(xa, k.L0, 0x0C020400u);
-  const uint32_t a1 = __builtin_amdgcn_perm(xa, k.L0, 0x0C020500u);
-  const uint32_t a2 = __builtin_amdgcn_perm(xa, k.L1, 0x0C020600u);
-  const uint32_t a3 = __builtin_amdgcn_perm(xa, k.L1, 0x0C020700u);
-  const uint32_t b0 = __builtin_amdgcn_perm(xb, k.L0, 0x0C020400u);
-  const uint32_t b1 = __builtin_amdgcn_perm(xb, k.L0, 0x0C020500u);
-  const uint32_t b2 = __builtin_amdgcn_perm(xb, k.L1, 0x0C020600u);
-  const uint32_t b3 = __builtin_amdgcn_perm(xb, k.L1, 0x0C020700u);
-  uint2 u0, u1, u2, u3, v0, v1, v2, v3;
-  asm volatile("ds_read_b64 %0, %1" : "=v"(u0) : "v"(a0));
-  asm volatile("ds_read_b64 %0, %1" : "=v"(u1) : "v"(a1));
-  asm volatile("ds_read_b64 %0, %1" : "=v"(u2) : "v"(a2));
-  asm volatile("ds_read_b64 %0, %1" : "=v"(u3) : "v"(a3));
-  asm volatile("ds_read_b64 %0, %1" : "=v"(v0) : "v"(b0));
-  asm volatile("ds_read_b64 %0, %1" : "=v"(v1) : "v"(b1));
-  asm volatile("ds_read_b64 %0, %1" : "=v"(v2) : "v"(b2));
-  asm volatile("ds_read_b64 %0, %1" : "=v"(v3) : "v"(b3));
-  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(u0), "+v"(u1), "+v"(u2), "+v"(u3), "+v"(v0), "+v"(v1), "+v"(v2),
-               "+v"(v3));
-  xa = xor3(xor3(u0.x, u1.y, u2.x), u3.y, wa);
-  xb = xor3(xor3(v0.x, v1.y, v2.x), v3.y, wb);
-}
-
-// Apply a uniform nibble-table map (8 x 16 entries at LDS byte offset `off`, broadcast reads).
-__device__ __forceinline__ uint32_t nibble_map_uniform(uint32_t s, const uint32_t* lds, uint32_t off);
-
-// Absorb one 128-byte line (8 x 16 B) into register s: bytes 0-63 continue the lane's chain, bytes
-// 64-127 start a fresh chain from 0; the two are joined with shift_64 (raw(A||B, s) =
-// shift_64(raw(A, s)) ^ raw(B, 0)). Two chains double the LDS reads in flight per wave.
-__device__ __forceinline__ uint32_t absorb_line(uint32_t s, const uint4 (&v)[8], const LaneCtx& k,
-                                                const uint32_t* lds) {
-  uint32_t xa = s ^ v[0].x, xb = v[4].x;
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    word4x2(xa, v[i].y, xb, v[4 + i].y, k);
-    word4x2(xa, v[i].z, xb, v[4 + i].z, k);
-    word4x2(xa, v[i].w, xb, v[4 + i].w, k);
-    word4x2(xa, i + 1 < 4 ? v[i + 1].x : 0u, xb, i + 1 < 4 ? v[5 + i].x : 0u, k);
-  }
-  return nibble_map_uniform(xa, lds, kLdsHalfOff) ^ xb;
-}
-
-// Apply a uniform nibble-table map (8 x 16 entries at LDS byte offset `off`, broadcast reads).
-__device__ __forceinline__ uint32_t nibble_map_uniform(uint32_t s, const uint32_t* lds, uint32_t off) {
-  const uint32_t* t = lds + off / 4;
-  uint32_t r[8];
-#pragma unroll
-  for (int k = 0; k < 8; k++) r[k] = t[k * 16 + __builtin_amdgcn_ubfe(s, 4 * k, 4)];
-  return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6] ^ r[7]);
-}
-
-// Lane-position join: shift_{(G-1-j)*128}(s) from the replicated nibble tables (slot = lane & 31).
-__device__ __forceinline__ uint32_t nibble_map_lane(uint32_t s, const uint32_t* lds, uint32_t slot4) {
-  const char* b = reinterpret_cast<const char*>(lds) + kLdsJoinOff;
-  uint32_t r[8];
-#pragma unroll
-  for (int k = 0; k < 8; k++)
-    r[k] = *reinterpret_cast<const uint32_t*>(b + k * 2048 + ((__builtin_amdgcn_ubfe(s, 4 * k, 4) << 7) | slot4));
-  return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6] ^ r[7]);
-}
-
-// xor-reduce across the G lanes of a lane-group; the value is complete on lane j = G-1.
-template <int G>
-__device__ __forceinline__ uint32_t group_xor_reduce(uint32_t x) {
-  if constexpr (G >= 2) x ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0xB1, 0xF, 0xF, false);   // quad_perm 1,0,3,2
-  if constexpr (G >= 4) x ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x4E, 0xF, 0xF, false);   // quad_perm 2,3,0,1
-  if constexpr (G >= 8) x ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x141, 0xF, 0xF, false);  // row_half_mirror
-  if constexpr (G >= 16) x ^= (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x140, 0xF, 0xF, false); // row_mirror
-  if constexpr (G >= 32)  // row_bcast15 into rows 1 and 3 only
-    x ^= (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x142, 0xA, 0xF, false);
-  return x;
-}
-
-// Stage the LDS image with LDS-DMA (global_load_lds_dwordx4): each wave-instruction moves 1 KiB
-// straight into LDS with no VGPR round trip, so the whole image is in flight at once.
-// Parts: slicing tables (img_slice), the per-G join/round tables (img_group) and, for the
-// variable-length kernel, the inverse-shift tables (img_extra).
-template <uint32_t kBytes = kLdsImageBytes, int BLK = kBlock>
-__device__ __forceinline__ void load_image(uint4* lds4, const uint4* __restrict__ img_common,
-                                           const uint4* __restrict__ img_group,
-                                           const uint4* __restrict__ img_extra = nullptr) {
-  constexpr int kCommon = kLdsCommonBytes / 16;
-  constexpr int kBase = kLdsImageBytes / 16;
-  constexpr int kTotal = kBytes / 16;
-  constexpr int kChunks = (kTotal + 63) / 64;  // 1 KiB pieces (the last one may be partial)
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int c = wave; c < kChunks; c += BLK / 64) {
-    const int i = c * 64 + lane;
-    if (i < kTotal) {
-      const uint4* src = i < kCommon ? img_common + i : (i < kBase ? img_group + (i - kCommon) : img_extra + (i - kBase));
-      __builtin_amdgcn_global_load_lds(src, lds4 + c * 64, 16, 0, 0);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
 
 // Fixed-length batch: payload p = base + p*stride, `len_blocks` 16-byte blocks, 16-byte aligned.
 // Chunks are aligned to the payload END (virtual leading zero blocks pad the first round), so every
@@ -246,27 +117,51 @@ __global__ __launch_bounds__(kBlock) void crc32_fixed_kernel(const uint8_t* __re
     advance(t_c, r_c);
   };
 
+  // unconditional loads (a step past the end re-reads step 0's line): see crc32_oneround_kernel
   for (size_t q = 0; q < nsteps; q += 2) {
-    if (q + 1 < nsteps) load_step(t_ld, r_ld, B);
+    {
+      const bool ok = q + 1 < nsteps;
+      load_step(ok ? t_ld : 0, ok ? r_ld : 0u, B);
+    }
     advance(t_ld, r_ld);
     __builtin_amdgcn_sched_barrier(0);
     compute_step(A);
-    if (q + 2 < nsteps) load_step(t_ld, r_ld, A);
+    {
+      const bool ok = q + 2 < nsteps;
+      load_step(ok ? t_ld : 0, ok ? r_ld : 0u, A);
+    }
     advance(t_ld, r_ld);
     __builtin_amdgcn_sched_barrier(0);
     if (q + 1 < nsteps) compute_step(B);
   }
 }
 
+// Arena-mode arguments (crc32_arena.hip). The main loop streams the arena's FULL
+// superblocks [fs0, fs1) as 1 KiB blocks (base = superblock fs0, stride 1 KiB, G = 8); the partial
+// superblocks at the two ends, if any, are done first by global waves 0 and 1, whose lanes outside
+// [line_lo, line_hi] read the zero line.
+struct ArenaOut {
+  uint32_t *c1, *c8, *c64;  // indexed from superblock sb0
+  uint64_t line_lo, line_hi, sb0, nsb, fs0, fs1;
+  uint64_t zero_line;
+};
+
 // Single-round fast path (payload = exactly G lines, 16-byte aligned; BASELINE config 1 is G = 8):
 // each step is one whole payload per lane-group, so there is no round state, and the per-lane line
 // pointer advances by a constant per task. Loads run one task ahead (A/B double buffer).
-template <int G, int BLK = kBlock, int VWG = kVwg>
+//   ARENA (G = 8): the arena line pass instead of digests - per line the raw CRC c1 (register 0, no
+//   init), per 1 KiB block the join c8, per 8 KiB superblock (the 8 groups of a wave) c64.
+//   PROBE (microbench only; product = 0, ARENA only): bit 0 drops the c1 store, bit 1 the superblock
+//   join - wrong outputs, used to measure what those stages cost.
+template <int G, int BLK = kBlock, int VWG = kVwg, bool ARENA = false, int PROBE = 0>
 __global__ __launch_bounds__(BLK) void crc32_oneround_kernel(const uint8_t* __restrict__ base, size_t n,
                                                                 size_t stride, const uint4* __restrict__ img_slice,
                                                                 const uint4* __restrict__ img_group,
-                                                                uint32_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsImageBytes / 16];
+                                                                uint32_t* __restrict__ out,
+                                                                const uint4* __restrict__ img_sb = nullptr,
+                                                                ArenaOut ar = {}) {
+  constexpr uint32_t kImage = ARENA ? kLdsArenaImageBytes : kLdsImageBytes;
+  __shared__ __attribute__((aligned(16))) uint4 lds4[kImage / 16];
   const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
 
   const uint32_t j = threadIdx.x & (G - 1);
@@ -279,7 +174,7 @@ __global__ __launch_bounds__(BLK) void crc32_oneround_kernel(const uint8_t* __re
   k.L0 = (threadIdx.x & 31) << 3;
   k.L1 = k.L0 | (1u << 16);
   k.slot4 = (threadIdx.x & 31) << 2;
-  const uint32_t sinit = j == 0 ? kInit : 0u;  // init == complement of the payload's first word
+  const uint32_t sinit = (!ARENA && j == 0) ? kInit : 0u;  // init == complement of the payload's first word
 
   const uint8_t* lp = base + gid * stride + (size_t)j * kChunkBytes;
   uint32_t* op = out + gid;
@@ -288,25 +183,69 @@ __global__ __launch_bounds__(BLK) void crc32_oneround_kernel(const uint8_t* __re
 #pragma unroll
     for (int i = 0; i < 8; i++) A[i] = reinterpret_cast<const uint4*>(lp)[i];
   }
-  load_image<kLdsImageBytes, BLK>(lds4, img_slice, img_group);
+  load_image<kImage, BLK>(lds4, img_slice, img_group, img_sb);
   __syncthreads();
 
-  auto finish = [&](uint32_t s) {
-    uint32_t t = s;
-    if constexpr (G > 1) t = group_xor_reduce<G>(nibble_map_lane(s, lds, k.slot4));
-    if (j == G - 1) *op = ~t;
-    op += ngroups;
+  const uint32_t lane = threadIdx.x & 63;
+  // arena mode: block index (relative to superblock sb0) of this group's current task
+  uint64_t blk = ARENA ? (ar.fs0 - ar.sb0) * 8 + gid : 0;
+  // Interleaved with the read stream, each written byte costs about five read bytes: the c1 array (3 %
+  // of the arena) costs ~14 % of the pass (microbench/arena_mb.hip).
+  auto arena_out = [&](uint32_t r, uint64_t b) {  // r = raw CRC of this lane's line, b = its block
+    if constexpr ((PROBE & 1) == 0) __builtin_nontemporal_store(r, ar.c1 + b * 8 + j);
+    const uint32_t t = group_xor_reduce<8>(nibble_map_lane(r, lds, k.slot4));  // complete on j == 7
+    uint32_t u = 0;
+    if (j == 7) {
+      ar.c8[b] = t;
+      if constexpr ((PROBE & 2) == 0) u = sb_join(t, lds, lane >> 3);
+    }
+    if constexpr ((PROBE & 2) == 0) {
+      u ^= __shfl_xor(u, 8, 64);
+      u ^= __shfl_xor(u, 16, 64);
+      u ^= __shfl_xor(u, 32, 64);
+      if (lane == 63) ar.c64[b >> 3] = u;
+    }
   };
+  if constexpr (ARENA) {
+    // partial superblocks at the arena ends (wave-uniform, two waves of the grid)
+    const uint64_t gw = (uint64_t)blockIdx.x * (BLK / 64) + (threadIdx.x >> 6);
+    if (gw < 2) {
+      const uint64_t sb = gw == 0 ? ar.sb0 : ar.sb0 + ar.nsb - 1;
+      if ((sb < ar.fs0 || sb >= ar.fs1) && (gw == 0 || sb != ar.sb0)) {
+        const uint64_t line = sb * 64 + lane;
+        const uint64_t src = line >= ar.line_lo && line <= ar.line_hi ? line << 7 : ar.zero_line;
+        uint4 v[8];
+#pragma unroll
+        for (int i = 0; i < 8; i++) v[i] = gload16(src + 16 * i);
+        arena_out(absorb_line(0u, v, k, lds), (sb - ar.sb0) * 8 + (lane >> 3));
+      }
+    }
+  }
+
+  auto finish = [&](uint32_t s) {
+    if constexpr (ARENA) {
+      arena_out(s, blk);
+      blk += ngroups;
+    } else {
+      uint32_t t = s;
+      if constexpr (G > 1) t = group_xor_reduce<G>(nibble_map_lane(s, lds, k.slot4));
+      if (j == G - 1) *op = ~t;
+      op += ngroups;
+    }
+  };
+  // Loads are unconditional (past the last task a group re-reads its current line, an L2 hit): with the
+  // next task's loads behind a branch the waitcnt pass merges the two paths and waits vmcnt(0) before
+  // every fold, which serialises the A/B double buffer.
   for (int t = 0; t < ntasks; t += 2) {
-    if (t + 1 < ntasks) {
-      const uint4* s = reinterpret_cast<const uint4*>(lp + pstep);
+    {
+      const uint4* s = reinterpret_cast<const uint4*>(t + 1 < ntasks ? lp + pstep : lp);
 #pragma unroll
       for (int i = 0; i < 8; i++) B[i] = s[i];
     }
     __builtin_amdgcn_sched_barrier(0);
     finish(absorb_line(sinit, A, k, lds));
-    if (t + 2 < ntasks) {
-      const uint4* s = reinterpret_cast<const uint4*>(lp + 2 * pstep);
+    {
+      const uint4* s = reinterpret_cast<const uint4*>(t + 2 < ntasks ? lp + 2 * pstep : lp);
 #pragma unroll
       for (int i = 0; i < 8; i++) A[i] = s[i];
     }
@@ -354,17 +293,6 @@ __device__ __forceinline__ VarTask decode_task(uint4 d, bool valid) {
   k.len = len;
   k.p = d.w;
   return k;
-}
-
-// 16-byte load through an address-space-1 pointer built from an integer address: the compiler
-// emits global_load_dwordx4 (vmcnt only) instead of flat_load (vmcnt + lgkmcnt, which would make
-// every LDS wait also wait for HBM).
-typedef unsigned int v4u32 __attribute__((ext_vector_type(4)));
-__device__ __forceinline__ uint32_t clamp032(int32_t x) { return (uint32_t)min(max(x, 0), 32); }  // v_med3_i32
-__device__ __forceinline__ uint4 gload16(uint64_t addr) {
-  const __attribute__((address_space(1))) v4u32* p = (const __attribute__((address_space(1))) v4u32*)addr;
-  const v4u32 x = *p;
-  return make_uint4(x.x, x.y, x.z, x.w);
 }
 
 // Branch-free descriptor fetch: past the end it re-reads the last entry (validity is tracked apart),
@@ -784,7 +712,31 @@ hipError_t launch_full(const FixedLaunch& a, hipStream_t stream) {
   }
 }
 
+template <int PROBE>
+hipError_t launch_arena_lines_p(const ArenaLaunch& a, hipStream_t stream) {
+  ArenaOut ar;
+  ar.c1 = a.c1;
+  ar.c8 = a.c8;
+  ar.c64 = a.c64;
+  ar.line_lo = a.line_lo;
+  ar.line_hi = a.line_hi;
+  ar.sb0 = a.sb0;
+  ar.nsb = a.nsb;
+  ar.fs0 = a.fs0;
+  ar.fs1 = a.fs1;
+  ar.zero_line = (uint64_t)(uintptr_t)a.zero_line;
+  const size_t nblk = (size_t)(a.fs1 - a.fs0) * 8;  // full 1 KiB blocks
+  const size_t blocks = std::max<size_t>(1, std::min<size_t>(a.max_blocks, (nblk * 8 + kBlock - 1) / kBlock));
+  hipLaunchKernelGGL((crc32_oneround_kernel<8, kBlock, kVwg, true, PROBE>), dim3((unsigned)blocks), dim3(kBlock), 0,
+                     stream, reinterpret_cast<const uint8_t*>((uintptr_t)(a.fs0 * 8192)), nblk, (size_t)1024,
+                     static_cast<const uint4*>(a.img_slice), static_cast<const uint4*>(a.img_group8), nullptr,
+                     static_cast<const uint4*>(a.img_sb), ar);
+  return hipGetLastError();
+}
+
 }  // namespace
+
+hipError_t launch_arena_lines(const ArenaLaunch& a, hipStream_t stream) { return launch_arena_lines_p<0>(a, stream); }
 
 hipError_t launch_fixed(const FixedLaunch& a, hipStream_t stream) {
   if (!a.raw && a.full && a.rounds == 1) return launch_one(a, stream);

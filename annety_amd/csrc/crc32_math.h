@@ -110,5 +110,17 @@ constexpr uint32_t kLdsUnshiftOff = kLdsImageBytes;
 constexpr uint32_t kLdsUnshiftBytes = 24 * 512;
 constexpr uint32_t kLdsVarImageBytes = kLdsUnshiftOff + kLdsUnshiftBytes;  // 160768 <= 163840
 constexpr uint32_t kChunkBytes = 128;  // one cache line per lane per round
+// Arena path (crc32_arena.hip), bulk line kernel: common + G=8 group part + superblock join
+//   [kLdsImageBytes, +4 KiB)  (k nibble, v value, g group) at k*512 + v*32 + g*4 = shift_{(7-g)*1024}(v << 4k)
+constexpr uint32_t kLdsSbJoinOff = kLdsImageBytes;
+constexpr uint32_t kLdsSbJoinBytes = 4096;
+constexpr uint32_t kLdsArenaImageBytes = kLdsSbJoinOff + kLdsSbJoinBytes;  // 152576
+// Arena path, stitch kernel: common + level maps + inverse shifts (no group part)
+//   [kLdsCommonBytes, +1.5 KiB)  level L = 0/1/2: (k, v) at L*512 + k*64 + v*4 = shift_{128*8^L}(v << 4k)
+//   [+1.5 KiB, +12 KiB)          U_lo[m] = shift_{-m}, U_hi[h] = shift_{-16h} (same layout as kLdsUnshiftOff)
+constexpr uint32_t kLdsLevelOff = kLdsCommonBytes;
+constexpr uint32_t kLdsLevelBytes = 3 * 512;
+constexpr uint32_t kLdsStitchUnshiftOff = kLdsLevelOff + kLdsLevelBytes;
+constexpr uint32_t kLdsStitchImageBytes = kLdsStitchUnshiftOff + kLdsUnshiftBytes;  // 145408
 
 }  // namespace annety_crc

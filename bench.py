@@ -38,6 +38,9 @@ def parse():
                    help="untimed seconds of launches before warmup (the GPU ramps its clocks on sustained load)")
     p.add_argument("--config", type=int, default=1, choices=[1, 2, 3],
                    help="BASELINE config: 1 = 1M x 1 KiB (headline), 2 = 4K x 4 MiB, 3 = Zipf 64 B-64 KiB (~1 GiB)")
+    p.add_argument("--var-path", choices=["arena", "sorted"], default="arena",
+                   help="config 3: arena = one pass over the packed arena + per-payload stitch (annety_crc32_batch_var_arena); "
+                        "sorted = the general length-bucketed path (annety_crc32_batch_var)")
     p.add_argument("--payloads", type=int, default=None, help="override payloads per GPU (fixed configs)")
     p.add_argument("--len", type=int, default=None, help="override payload bytes (fixed configs)")
     p.add_argument("--e2e", action="store_true",
@@ -97,7 +100,10 @@ class Workload:
             self.lengths = torch.from_numpy(lens.astype(np.int32)).to(dev)
             self.payload_bytes = total
             self.algo_bytes = total + 4 * self.n + 12 * self.n  # + offset/length metadata reads
-            self.kernel = "crc32_var_kernel<8> (annety_amd/csrc/crc32_kernels.hip)"
+            self.arena = args.var_path == "arena"
+            self.kernel = ("crc32_arena_lines_kernel + crc32_arena_stitch_kernel (annety_amd/csrc/crc32_arena.hip)"
+                           if self.arena else
+                           "crc32_bucket_hist/scan/scatter + crc32_var_kernel<32/8/2> (annety_amd/csrc/crc32_kernels.hip)")
             self.desc = (f"BASELINE config 3: {self.n} payloads, Zipf(1.1) lengths 64 B-64 KiB packed unaligned, "
                          f"{total / 2**30:.3f} GiB per GPU")
         self.out = torch.empty(self.n, dtype=torch.int32, device=dev)
@@ -108,7 +114,8 @@ class Workload:
         if self.config in (1, 2):
             annety_amd.crc32_batch(self.data, self.n, self.L, out=self.out, stream=stream_handle)
         else:
-            annety_amd.crc32_batch_var(self.data, self.offsets, self.lengths, out=self.out, stream=stream_handle)
+            annety_amd.crc32_batch_var(self.data, self.offsets, self.lengths, out=self.out, stream=stream_handle,
+                                       arena=True if self.arena else None)
 
     def host_sample(self, max_bytes=4 << 20):
         """(host bytes, offsets, lengths) of a bounded prefix of the batch, for the oracle legs."""

@@ -24,7 +24,7 @@
 extern "C" {
 #endif
 
-#define ANNETY_CRC_ABI_VERSION 1
+#define ANNETY_CRC_ABI_VERSION 2
 
 enum {
   ANNETY_CRC_OK = 0,
@@ -82,6 +82,18 @@ int annety_crc32_update_batch_fixed(uint32_t* d_state, const void* d_base, size_
 int annety_crc32_update_batch_var(uint32_t* d_state, const void* d_base, const uint64_t* d_off, const uint32_t* d_len,
                                   size_t n, void* stream);
 
+/* Arena variants of the two entry points above, for payloads that lie in one buffer of arena_bytes
+ * bytes at d_arena (a NetBuffer's readable bytes, a frame stream, a packed batch; offsets are relative
+ * to d_arena). One pass streams every 128-byte line of the arena whatever the length mix, then one lane
+ * per payload joins its lines, so the cost follows arena_bytes: use these when the
+ * payloads cover most of the arena, and the two entry points above for sparse batches. A payload that
+ * reaches outside [0, arena_bytes) is still computed correctly (its lines are folded directly).
+ * Same results and argument rules as annety_crc32_batch_var / annety_crc32_update_batch_var. */
+int annety_crc32_batch_var_arena(const void* d_arena, size_t arena_bytes, const uint64_t* d_off,
+                                 const uint32_t* d_len, size_t n, uint32_t* d_out, void* stream);
+int annety_crc32_update_batch_var_arena(uint32_t* d_state, const void* d_arena, size_t arena_bytes,
+                                        const uint64_t* d_off, const uint32_t* d_len, size_t n, void* stream);
+
 /* ---- host-memory batch (payloads off a NetBuffer/socket): staged through pinned buffers, H2D ->
  * kernel -> D2H, pipelined on two streams. Synchronous. ---- */
 int annety_crc32_batch_fixed_host(const void* h_base, size_t n, size_t len, size_t stride, uint32_t* h_out);
@@ -104,6 +116,11 @@ int annety_lhc_parse(const void* h_stream, size_t size, int length_type, int64_t
  * d_digest (optional, may be NULL) receives the computed CRCs. */
 int annety_lhc_verify_batch(const void* d_stream, const uint64_t* d_payload_off, const uint32_t* d_payload_len,
                             size_t n, uint8_t* d_ok, uint32_t* d_digest, void* stream);
+/* Same as annety_lhc_verify_batch over the arena path: d_stream holds stream_bytes bytes (the received
+ * stream the frames were parsed from), so the payload CRCs take one pass over the stream. */
+int annety_lhc_verify_stream(const void* d_stream, size_t stream_bytes, const uint64_t* d_payload_off,
+                             const uint32_t* d_payload_len, size_t n, uint8_t* d_ok, uint32_t* d_digest,
+                             void* stream);
 /* Host plan for a batch of LengthHeaderCodec::encode calls (:169-176): h_rt[i] (optional) = 1, or 0 for
  * an empty payload, or -1 for len > max_payload (max_payload > 0); h_frame_off[i] = where frame i starts
  * when the frames of accepted payloads are packed back to back (rejected ones take no bytes);

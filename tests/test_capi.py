@@ -46,13 +46,17 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version_and_errors():
     lib = _lib.get()
-    assert lib.annety_crc_abi_version() == 1
+    want = int(re.search(r"#define ANNETY_CRC_ABI_VERSION (\d+)", open(HEADER).read()).group(1))
+    assert lib.annety_crc_abi_version() == want
     assert lib.annety_crc_strerror(-1) == b"invalid argument"
     # argument errors are reported before any device is touched
     assert lib.annety_crc32_batch_fixed(None, 4, 16, 16, None, None) == -1
     assert lib.annety_crc32_batch_fixed(None, 0, 16, 16, None, None) == 0  # empty batch is a no-op
     assert lib.annety_crc32_batch_var(None, None, None, 3, None, None) == -1
     assert lib.annety_crc32_batch_fixed_host(None, 2, 16, 8, None) == -1  # stride < len
+    assert lib.annety_crc32_batch_var_arena(None, 64, None, None, 3, None, None) == -1
+    assert lib.annety_crc32_update_batch_var_arena(None, None, 64, None, None, 0, None) == 0
+    assert lib.annety_lhc_verify_stream(None, 64, None, None, 2, None, None, None) == -1
 
 
 def test_host_scalar_api_matches_reference(golden):

@@ -53,6 +53,11 @@ def test_config3_full_bitexact(gpu):
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, f"{bad.size} digest mismatches, first {bad[:8]} (lengths {lens[bad[:8]]})"
 
+    got = _u32(annety_amd.crc32_batch_var(data, d_off, d_len, arena=True))
+    print("config 3: arena digests done", flush=True)
+    bad = np.nonzero(got != want)[0]
+    assert bad.size == 0, f"arena path: {bad.size} digest mismatches, first {bad[:8]} (lengths {lens[bad[:8]]})"
+
     rng = np.random.default_rng(3)
     states = rng.integers(0, 2 ** 32, lens.size, dtype=np.uint64).astype(np.uint32)
     d_state = torch.from_numpy(states.view(np.int32).copy()).to(gpu)
@@ -62,6 +67,10 @@ def test_config3_full_bitexact(gpu):
     want = oracle.batch_var_mt(host, offs, lens, THREADS, states=states)
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, f"{bad.size} register mismatches, first {bad[:8]}"
+    d_state = torch.from_numpy(states.view(np.int32).copy()).to(gpu)
+    annety_amd.crc32_update_batch_var(d_state, data, d_off, d_len, arena=True)
+    bad = np.nonzero(_u32(d_state) != want)[0]
+    assert bad.size == 0, f"arena path: {bad.size} register mismatches, first {bad[:8]}"
 
 
 def test_config2_full_bitexact(gpu):
