@@ -34,6 +34,12 @@ SIGNATURES = [
     ("annety_crc32_batch_var_arena", ctypes.c_int, [_vp, _c_size, _vp, _vp, _c_size, _vp, _vp]),
     ("annety_crc32_update_batch_var_arena", ctypes.c_int, [_vp, _vp, _c_size, _vp, _vp, _c_size, _vp]),
     ("annety_crc32_batch_fixed_host", ctypes.c_int, [_vp, _c_size, _c_size, _c_size, _vp]),
+    ("annety_crc_shard_plan", ctypes.c_int, [_c_size, ctypes.c_int, _vp, _vp]),
+    ("annety_crc_group_create", ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(_vp)]),
+    ("annety_crc_group_destroy", ctypes.c_int, [_vp]),
+    ("annety_crc_group_size", ctypes.c_int, [_vp]),
+    ("annety_crc32_group_batch_fixed", ctypes.c_int, [_vp, _vp, _vp, _c_size, _c_size, _vp, _c_size]),
+    ("annety_crc32_group_batch_fixed_host", ctypes.c_int, [_vp, _vp, _c_size, _c_size, _c_size, _vp]),
     ("annety_lhc_parse", ctypes.c_int, [_vp, _c_size, ctypes.c_int, ctypes.c_int64, _vp, _vp, _c_size,
                                         ctypes.POINTER(_c_size), ctypes.POINTER(_c_size)]),
     ("annety_lhc_verify_batch", ctypes.c_int, [_vp, _vp, _vp, _c_size, _vp, _vp, _vp]),

@@ -14,9 +14,10 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(ROOT, "include")
 LIB = os.path.join(PKG, "libannety_crc.so")
-SOURCES = ["crc32_kernels.hip", "crc32_arena.hip", "crc32_frames.hip", "crc32_capi.cpp"]
+SOURCES = ["crc32_kernels.hip", "crc32_arena.hip", "crc32_frames.hip", "crc32_capi.cpp", "crc32_group.cpp"]
 HEADERS = ["crc32_kernels.h", "crc32_math.h", "crc32_device.h"]
 ARCH = "gfx950"
+ROCM_LIB = "/opt/rocm/lib"
 
 
 def hipcc() -> str:
@@ -57,7 +58,10 @@ def build(force: bool = False, verbose: bool = False) -> str:
         subprocess.run(cmd, check=True)
         objs.append(obj)
     out_tmp = LIB + ".tmp"
-    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out_tmp] + objs
+    # RCCL for the device-group entry points (crc32_group.cpp); rpath so the library loads without
+    # LD_LIBRARY_PATH on any box with this ROCm image
+    cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out_tmp] + objs + [
+        f"-L{ROCM_LIB}", "-lrccl", f"-Wl,-rpath,{ROCM_LIB}"]
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)

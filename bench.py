@@ -1,21 +1,31 @@
 #!/usr/bin/env python3
-"""Headline benchmark: device-resident CRC-32 (annety's "Crc32c") over 1M x 1 KiB payloads per GPU.
+"""Headline benchmark: device-resident CRC-32 (annety's "Crc32c") over 1 KiB payloads per GPU.
 
 BASELINE.json metric: "CRC-32C GiB/s device-resident (1M x 1KiB) @1/2/4/8 MI355X; % HBM roofline".
-A step = one batch launch over the GPU's payloads already resident in HBM. The default workload is
-BASELINE config 1 (1M x 1 KiB per GPU); --config 2 / 3 run the other single-GPU configs (4K x 4 MiB,
-Zipf-mixed lengths) as secondary lines. N GPUs = N ranks (torch.distributed.run), each with its own
-shard of the same size (weak scaling, no data-path collective: payloads are independent). After the
-timed region the per-shard digests are gathered to rank 0 once over RCCL (gather_ms, not in `value`).
+A step = one pass of the hot path over the GPU's batch, already resident in HBM.
+
+  * N = 1 (default): BASELINE config 1, 1M x 1 KiB, one batch launch per step.
+  * N > 1: BASELINE config 4's per-GPU shard, 8M x 1 KiB (8 GiB) per rank, weak scaling. A step
+    checksums the shard in chunks and gathers each chunk's digests to rank 0 over RCCL/xGMI while
+    the next chunk is computed (annety_amd.sharded.PipelinedGather) - the gather is inside `value`;
+    `value_compute_only` is the same step without it.
+  * --config 2 / 3 run the other single-GPU configs (4K x 4 MiB; Zipf 64 B-64 KiB packed, arena path)
+    as secondary lines.
+
+`python bench.py --gpus N` with N > 1 and no torchrun environment spawns the N ranks itself (one
+process per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR=127.0.0.1), before anything touches the GPU;
+under torch.distributed.run it uses the launcher's ranks. Prints ONE JSON line on rank 0
+(contract: DESIGN.md §4).
 
 Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C] [--e2e] [--no-cpu]
-Prints ONE JSON line on rank 0 (contract: DESIGN.md §4).
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -26,7 +36,11 @@ sys.path.insert(0, ROOT)
 
 METRIC = "CRC-32C GiB/s device-resident (1M×1KiB) @1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md (8.0 TB/s)
-PMC_FILE = os.path.join(ROOT, "profiles", "r01_pmc_traffic.json")
+# Per-launch HBM bytes measured by profiles/pmc.sh at this code (FETCH_SIZE x2 + WRITE_SIZE), per config.
+PMC_FILES = {1: "profiles/r02/config1_pmc.json", 3: "profiles/r02/config3_arena_pmc.json",
+             2: "profiles/r02/config2_pmc.json", 4: "profiles/r02/config1_pmc.json"}
+# The reference build of oracle/_ref (oracle/Makefile): the reference's Release flags without -march=native.
+REF_FLAGS = "g++ -std=c++11 -O2 -DNDEBUG (CMakeLists.txt:24,48 Release flags; -march=native dropped so the .so runs on any host)"
 
 
 def parse():
@@ -36,11 +50,13 @@ def parse():
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--prewarm-s", type=float, default=1.0,
                    help="untimed seconds of launches before warmup (the GPU ramps its clocks on sustained load)")
-    p.add_argument("--config", type=int, default=1, choices=[1, 2, 3],
-                   help="BASELINE config: 1 = 1M x 1 KiB (headline), 2 = 4K x 4 MiB, 3 = Zipf 64 B-64 KiB (~1 GiB)")
+    p.add_argument("--config", type=int, default=None, choices=[1, 2, 3, 4],
+                   help="BASELINE config: 1 = 1M x 1 KiB (N=1 default), 2 = 4K x 4 MiB, 3 = Zipf 64 B-64 KiB (~1 GiB), "
+                        "4 = 8M x 1 KiB per GPU + pipelined RCCL gather (N>1 default)")
     p.add_argument("--var-path", choices=["arena", "sorted"], default="arena",
                    help="config 3: arena = one pass over the packed arena + per-payload stitch (annety_crc32_batch_var_arena); "
                         "sorted = the general length-bucketed path (annety_crc32_batch_var)")
+    p.add_argument("--chunks", type=int, default=8, help="config 4: chunks per shard for the pipelined gather")
     p.add_argument("--payloads", type=int, default=None, help="override payloads per GPU (fixed configs)")
     p.add_argument("--len", type=int, default=None, help="override payload bytes (fixed configs)")
     p.add_argument("--e2e", action="store_true",
@@ -48,6 +64,31 @@ def parse():
     p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample duration")
     return p.parse_args()
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn(n: int, argv=None) -> int:
+    """Start n ranks of `argv` (default: this script with the same arguments), one per GPU, the way
+    torch.distributed.run would, and wait; nothing here touches the GPU. Rank 0's stdout (the JSON line)
+    passes through; the exit status is the worst of the ranks'."""
+    argv = argv if argv is not None else [os.path.abspath(__file__)] + sys.argv[1:]
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable] + list(argv), env=env,
+                                      stdout=None if r == 0 else subprocess.DEVNULL))
+    rcs = [p.wait() for p in procs]
+    return max(rcs, key=lambda c: abs(c))
 
 
 def zipf_batch(seed: int, target: int = 1 << 30):
@@ -79,18 +120,27 @@ class Workload:
         gen = torch.Generator(device=dev)
         gen.manual_seed(0xC0FFEE + 7919 * rank + args.config)
         self.config = args.config
-        if args.config in (1, 2):
-            n = args.payloads or (1 << 20 if args.config == 1 else 4096)
-            L = args.len or (1024 if args.config == 1 else 4 << 20)
+        self.arena = False
+        if args.config in (1, 2, 4):
+            default_n = {1: 1 << 20, 2: 4096, 4: 8 << 20}[args.config]
+            n = args.payloads or default_n
+            L = args.len or (4 << 20 if args.config == 2 else 1024)
             self.n, self.L = n, L
             self.data = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev, generator=gen)
             self.payload_bytes = n * L
             self.algo_bytes = n * L + 4 * n  # payload reads + digest writes per launch
             self.offsets = self.lengths = None
-            self.kernel = ("crc32_oneround_kernel<8>" if L == 1024 else "crc32_fixed_kernel") + \
-                " (annety_amd/csrc/crc32_kernels.hip)"
-            self.desc = (f"BASELINE config {args.config}: {n} x {L} B payloads contiguous in HBM per GPU, "
-                         "one batch launch per step")
+            if args.config == 2:
+                self.kernel = "crc32_fixed_kernel<32> over 64 KiB segments + crc32_split_join (annety_amd/csrc/crc32_kernels.hip)"
+            else:
+                self.kernel = "crc32_oneround_kernel<8> (annety_amd/csrc/crc32_kernels.hip)"
+            if args.config == 4:
+                self.desc = (f"BASELINE config 4 shard: {n} x {L} B payloads per GPU (64M x 1 KiB at 8 GPUs), "
+                             f"{args.chunks} chunks per step, each chunk's digests gathered to rank 0 over RCCL "
+                             "while the next chunk is computed")
+            else:
+                self.desc = (f"BASELINE config {args.config}: {n} x {L} B payloads contiguous in HBM per GPU, "
+                             "one batch launch per step")
         else:
             lens, offs = zipf_batch(0x5EED + rank)
             total = int(lens.sum())
@@ -101,25 +151,29 @@ class Workload:
             self.payload_bytes = total
             self.algo_bytes = total + 4 * self.n + 12 * self.n  # + offset/length metadata reads
             self.arena = args.var_path == "arena"
-            self.kernel = ("crc32_arena_lines_kernel + crc32_arena_stitch_kernel (annety_amd/csrc/crc32_arena.hip)"
-                           if self.arena else
-                           "crc32_bucket_hist/scan/scatter + crc32_var_kernel<32/8/2> (annety_amd/csrc/crc32_kernels.hip)")
+            self.kernel = ("crc32_oneround_kernel<8, arena> + crc32_arena_stitch_kernel, one step "
+                           "(annety_amd/csrc/crc32_kernels.hip, crc32_arena.hip)" if self.arena else
+                           "crc32_bucket_hist/scan/scatter + crc32_var_kernel<32/8/2>, one step "
+                           "(annety_amd/csrc/crc32_kernels.hip)")
             self.desc = (f"BASELINE config 3: {self.n} payloads, Zipf(1.1) lengths 64 B-64 KiB packed unaligned, "
-                         f"{total / 2**30:.3f} GiB per GPU")
+                         f"{total / 2**30:.3f} GiB per GPU, " + ("arena path" if self.arena else "sorted path"))
         self.out = torch.empty(self.n, dtype=torch.int32, device=dev)
 
-    def launch(self, stream_handle):
+    def launch(self, stream_handle, lo: int = 0, hi: int | None = None):
+        """Digests of payloads [lo, hi) into self.out[lo:hi] (fixed configs); the whole batch otherwise."""
         import annety_amd
 
-        if self.config in (1, 2):
-            annety_amd.crc32_batch(self.data, self.n, self.L, out=self.out, stream=stream_handle)
-        else:
-            annety_amd.crc32_batch_var(self.data, self.offsets, self.lengths, out=self.out, stream=stream_handle,
-                                       arena=True if self.arena else None)
+        if self.config in (1, 2, 4):
+            hi = self.n if hi is None else hi
+            annety_amd.crc32_batch(self.data[lo * self.L:], hi - lo, self.L, out=self.out[lo:hi], stream=stream_handle)
+            return self.out[lo:hi]
+        annety_amd.crc32_batch_var(self.data, self.offsets, self.lengths, out=self.out, stream=stream_handle,
+                                   arena=True if self.arena else None)
+        return self.out
 
     def host_sample(self, max_bytes=4 << 20):
         """(host bytes, offsets, lengths) of a bounded prefix of the batch, for the oracle legs."""
-        if self.config in (1, 2):
+        if self.config in (1, 2, 4):
             ns = max(1, min(self.n, max_bytes // self.L))
             h = self.data[: ns * self.L].cpu().numpy()
             return h, np.arange(ns, dtype=np.uint64) * self.L, np.full(ns, self.L, dtype=np.uint32)
@@ -139,7 +193,8 @@ def cpu_baseline(h: np.ndarray, offs: np.ndarray, lens: np.ndarray, budget_s: fl
 
     import oracle
 
-    threads = max(1, min(16, os.cpu_count() or 1))  # the box's CPU share for one GPU
+    host_cpus = os.cpu_count() or 1
+    threads = max(1, min(16, host_cpus))  # the GPU box's CPU share for one GPU (16 of the machine's cores)
     n = len(offs)
     L0 = int(lens[0])
     fixed = bool(np.all(lens == L0)) and bool(np.all(offs == np.arange(n, dtype=np.uint64) * L0))
@@ -157,14 +212,9 @@ def cpu_baseline(h: np.ndarray, offs: np.ndarray, lens: np.ndarray, budget_s: fl
             oracle.batch_fixed_mt(h, n, L0, threads=th)
     else:
         kind = "port"
-        parts = np.array_split(np.arange(n), threads)
 
         def run(th):
-            if th == 1:
-                oracle.batch_var(h, offs, lens)
-            else:  # ctypes releases the GIL: one oracle call per thread over its share of payloads
-                with cf.ThreadPoolExecutor(th) as ex:
-                    list(ex.map(lambda ix: oracle.batch_var(h, offs[ix], lens[ix]), parts))
+            oracle.batch_var_mt(h, offs, lens, th)
 
     def rate(th, budget):
         reps, t0 = 0, time.perf_counter()
@@ -181,24 +231,33 @@ def cpu_baseline(h: np.ndarray, offs: np.ndarray, lens: np.ndarray, budget_s: fl
         "value": round(mt_rate, 3),
         "unit": "GiB/s",
         "cores": threads,
+        "host_cpus": host_cpus,
         "kind": kind,
+        "compile_flags": REF_FLAGS if kind == "reference" else "gcc -O2 (oracle/Makefile, C restatement)",
         "single_thread_value": round(st_rate, 3),
         "sample": f"{n} payloads / {nbytes / 2**20:.1f} MiB prefix of the GPU workload copied to host, crc32_long "
                   f"per payload, payload-parallel over {threads} threads x {mt_reps} passes (+ 1 thread x {st_reps})",
     }
 
 
-def pmc_traffic(w: Workload):
-    """Per-launch HBM bytes from the committed rocprofv3 PMC summary of this workload (FETCH_SIZE x2
-    gfx950 correction + WRITE_SIZE), or None if no matching profile is committed."""
+def pmc_traffic(w: Workload, var_path: str):
+    """Per-launch HBM bytes of this workload's kernels from the committed rocprofv3 PMC summary
+    (profiles/pmc.sh + pmc.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), summed over the kernels
+    of one step, or None if no summary for this configuration is committed."""
+    path = PMC_FILES.get(w.config)
+    if not path or (w.config == 3 and var_path != "arena") or (w.config in (1, 4) and w.L != 1024):
+        return None
     try:
-        with open(PMC_FILE) as f:
+        with open(os.path.join(ROOT, path)) as f:
             d = json.load(f)
-        if w.config == 1 and d.get("payloads") == w.n and d.get("len") == w.L:
-            return d.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
-        pass
-    return None
+        return None
+    tot = sum(v.get("hbm_bytes_per_launch", 0) for k, v in d.items() if "crc32_" in k)
+    if not tot:
+        return None
+    if w.config == 4:  # the config-1 measurement is per 1M payloads; a config-4 step is n/1M of them
+        tot = int(tot * w.n / (1 << 20))
+    return tot
 
 
 def e2e_host_path(w: Workload):
@@ -220,15 +279,22 @@ def e2e_host_path(w: Workload):
     ok = bool(np.array_equal(d, w.out.cpu().numpy().view(np.uint32)))
     return {"value": round(w.payload_bytes / dt / 2 ** 30, 2), "unit": "GiB/s", "ms_per_batch": round(dt * 1e3, 2),
             "bit_exact_vs_device_path": ok,
-            "path": "pageable host buffer -> pinned 64 MiB x2 ring -> hipMemcpyAsync H2D -> kernel -> D2H, 2 streams"}
+            "path": "pageable host buffer -> pinned 64 MiB x2 ring (multi-threaded pack) -> hipMemcpyAsync H2D -> "
+                    "kernel -> D2H, 2 streams"}
 
 
 def main():
     args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "0"))
+    if world == 0 and args.gpus > 1:
+        return spawn(args.gpus)  # before anything touches the GPU
+    world = max(world, 1)
+    if args.config is None:
+        args.config = 4 if world > 1 else 1
+
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
@@ -237,63 +303,76 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     import oracle
+    from annety_amd import sharded
 
     w = Workload(args, dev, rank)
     stream = torch.cuda.current_stream(dev)
     sh = int(stream.cuda_stream)
+    pipe = sharded.PipelinedGather(w.n, args.chunks, dst=0, device=dev) if world > 1 else None
 
-    # correctness gate before timing: bit-exact vs the oracle on a prefix of this rank's batch
-    w.launch(sh)
+    def step(gather: bool = True):
+        if pipe is None:
+            w.launch(sh)
+            return []
+        return pipe.run(lambda lo, hi: w.launch(sh, lo, hi), gather=gather)
+
+    # correctness gate before timing: bit-exact vs the oracle on a prefix of this rank's batch, and (N > 1)
+    # every rank's digests delivered to rank 0 intact (checksum of checksums)
+    sharded.PipelinedGather.wait(step())
     torch.cuda.synchronize()
     hs, ho, hl = w.host_sample()
     want = oracle.batch_var(hs, ho, hl)
     got = w.out[: len(ho)].cpu().numpy().view(np.uint32)
     if not np.array_equal(got, want):
         raise SystemExit(f"rank {rank}: digests differ from the oracle on the sample")
+    gather_ok = sharded.verify_gather(pipe.recv, w.out) if pipe is not None else None
+    if gather_ok is False:
+        raise SystemExit(f"rank {rank}: gathered digests differ from the ranks' own")
+
+    def timed(steps: int, gather: bool) -> float:
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            sharded.PipelinedGather.wait(step(gather))
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:  # max over ranks
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
 
     t_pw = time.perf_counter()
     while time.perf_counter() - t_pw < args.prewarm_s:
-        for _ in range(10):
-            w.launch(sh)
+        for _ in range(10 if world == 1 else 1):
+            step(gather=False)
         torch.cuda.synchronize()
     for _ in range(args.warmup):
-        w.launch(sh)
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    if world > 1:
-        dist.barrier()
+        sharded.PipelinedGather.wait(step())
     torch.cuda.synchronize()
-    t0 = time.perf_counter()
+
+    # kernel-only time on the launch stream (HIP events around the same number of steps, no gather)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ev0.record(stream)
     for _ in range(args.steps):
-        w.launch(sh)
+        step(gather=False)
     ev1.record(stream)
     torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    kern_ms = ev0.elapsed_time(ev1) / args.steps  # HIP events on the launch stream over the timed region
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
 
-    # one-shot RCCL gather of per-shard digests to rank 0 (not part of `value`)
-    gather_ms = None
-    if world > 1:
-        from annety_amd import sharded
-
-        torch.cuda.synchronize()
-        dist.barrier()
-        g0 = time.perf_counter()
-        sharded.gather_digests(w.out, [w.n] * world, dst=0)
-        torch.cuda.synchronize()
-        gather_ms = (time.perf_counter() - g0) * 1e3
+    elapsed = timed(args.steps, gather=True)
+    compute_only = timed(args.steps, gather=False) if world > 1 else None
 
     if rank == 0:
         total_gib = w.payload_bytes * world * args.steps / 2 ** 30
         achieved = w.algo_bytes / (kern_ms / 1e3) / 1e9
+        metric = METRIC if args.config in (1, 4) else METRIC.replace("(1M×1KiB)", f"(config {args.config})")
         line = {
-            "metric": METRIC if args.config == 1 else METRIC.replace("(1M×1KiB)", f"(config {args.config})"),
+            "metric": metric,
             "value": round(total_gib / elapsed, 2),
             "unit": "GiB/s",
             "n_gpus": world,
@@ -303,7 +382,7 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u8",
+            "dtype": "u32",
             "data": "synthetic (torch.randint bytes on device, seeded per rank)",
             "config": {
                 "workload": w.desc,
@@ -318,21 +397,26 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": pmc_traffic(w),
+                "traffic": pmc_traffic(w, args.var_path),
                 "kernel": w.kernel,
                 "kernel_ms_avg": round(kern_ms, 4),
                 "algorithmic_bytes_per_launch": w.algo_bytes,
             },
-            "cpu_baseline": None if args.no_cpu else cpu_baseline(hs, ho, hl, args.cpu_seconds),
+            "cpu_baseline": None if (args.no_cpu or world > 1) else cpu_baseline(hs, ho, hl, args.cpu_seconds),
         }
-        if gather_ms is not None:
-            line["gather_ms"] = round(gather_ms, 3)
-        if args.e2e:
+        if world > 1:
+            line["rccl_ranks"] = dist.get_world_size()
+            line["backend"] = dist.get_backend()
+            line["gather"] = {"chunks": len(pipe.bounds), "bytes_to_rank0_per_step": 4 * w.n * (world - 1),
+                              "verified": bool(gather_ok), "overlapped_with_compute": True}
+            line["value_compute_only"] = round(total_gib / compute_only, 2)
+        if args.e2e and world == 1:
             line["e2e_host_path"] = e2e_host_path(w)
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -98,6 +98,33 @@ int annety_crc32_update_batch_var_arena(uint32_t* d_state, const void* d_arena, 
  * kernel -> D2H, pipelined on two streams. Synchronous. ---- */
 int annety_crc32_batch_fixed_host(const void* h_base, size_t n, size_t len, size_t stride, uint32_t* h_out);
 
+/* ---- device groups: one process, several gfx950 devices ----
+ * A group is an RCCL communicator over `devices` (ncclCommInitAll, single process) plus a compute and a
+ * communication stream per device. Payloads are independent, so a batch shards into contiguous blocks
+ * with no data-path collective; the only exchange is the digests' trip to the root device (devices[0]).
+ * The C++ callers of annety (one process, N event loops: src/EventLoopPool.cc:55-66) use these to spread
+ * a batch over the GPUs of a node without torch.distributed. */
+typedef struct annety_crc_group annety_crc_group;
+/* Contiguous block shards of n payloads over nshards: shard k = [first[k], first[k] + count[k]), sizes
+ * within one of each other. Host only (no device needed). */
+int annety_crc_shard_plan(size_t n, int nshards, size_t* first, size_t* count);
+/* ANNETY_CRC_ENODEV if a device is missing or not gfx950, ANNETY_CRC_EINVAL for a repeated device,
+ * ANNETY_CRC_ERCCL if the communicator cannot be built. */
+int annety_crc_group_create(const int* devices, int ndev, annety_crc_group** out);
+int annety_crc_group_destroy(annety_crc_group* group);
+int annety_crc_group_size(const annety_crc_group* group);
+/* Device-resident shards: device k (the group's k-th) holds n_shard[k] payloads of len bytes at
+ * d_shard[k] (stride apart, memory of device k). d_root_out (memory of devices[0]) receives all
+ * sum(n_shard) digests in device order. Each shard is checksummed in `chunks` pieces and piece c's
+ * digests travel to the root (RCCL send/recv over xGMI) while piece c+1 is computed. Synchronous;
+ * ANNETY_CRC_ERCCL on a collective failure. */
+int annety_crc32_group_batch_fixed(annety_crc_group* group, const void* const* d_shard, const size_t* n_shard,
+                                   size_t len, size_t stride, uint32_t* d_root_out, size_t chunks);
+/* Host-memory batch spread over the group: payload shard k (annety_crc_shard_plan) is staged over device
+ * k's own PCIe link and checksummed there, all devices at once; h_out[i] = crc32_long(payload i). */
+int annety_crc32_group_batch_fixed_host(annety_crc_group* group, const void* h_base, size_t n, size_t len,
+                                        size_t stride, uint32_t* h_out);
+
 /* ---- LengthHeaderCodec wire format, batched ----
  * frame = [length: T bytes big-endian, T = 1/2/4/8][payload: length-4 bytes][crc32(payload): 4 bytes BE]
  * (include/codec/LengthHeaderCodec.h:33-46; decode :71-137; encode :146-201; checksum enabled). */

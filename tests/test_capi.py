@@ -138,3 +138,30 @@ def test_reference_codec_compiles_against_dropin(tmp_path):
     r = subprocess.run(["g++", "-std=c++11", "-fsyntax-only", f"-I{ROOT}/include/annety", f"-I{ROOT}/include",
                         "-I/root/reference/include", "-I/root/reference/src", str(src)], capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-3000:]
+
+
+def test_shard_plan_through_cabi():
+    """annety_crc_shard_plan (the C-ABI's shard arithmetic for device groups) against shard_range."""
+    from annety_amd import sharded
+
+    for n in [0, 1, 7, 1000, 1001, (64 << 20), (1 << 40) + 3]:
+        for k in [1, 2, 3, 8]:
+            plan = sharded.shard_plan(n, k)
+            assert [(f, f + c) for f, c in plan] == [sharded.shard_range(n, r, k) for r in range(k)]
+    lib = _lib.get()
+    assert lib.annety_crc_shard_plan(10, 0, None, None) == -1
+
+
+def test_group_errors_without_device():
+    """Group creation validates arguments before touching RCCL; with no GPU it reports ENODEV."""
+    import ctypes
+
+    lib = _lib.get()
+    h = ctypes.c_void_p()
+    assert lib.annety_crc_group_create(None, 1, ctypes.byref(h)) == -1
+    devs = (ctypes.c_int * 2)(0, 0)
+    rc = lib.annety_crc_group_create(devs, 2, ctypes.byref(h))
+    assert rc in (-1, -4)  # repeated device (EINVAL) or no device (ENODEV)
+    assert lib.annety_crc_group_size(None) == 0
+    assert lib.annety_crc_group_destroy(None) == 0
+    assert lib.annety_crc32_group_batch_fixed(None, None, None, 16, 16, None, 1) == -1

@@ -1,9 +1,13 @@
-"""Multi-process (world_size 2, gloo on CPU) coverage of the sharding path: shard ranges, the digest
-gather to rank 0 and the combine-joined stream CRC. The per-shard compute is the GPU kernel on a
-real run; here each rank uses the CPU oracle as the stand-in producer of its shard's digests, so the
-test checks the distributed plumbing, not the kernel."""
+"""Multi-process (world_size 2, gloo on CPU) coverage of the sharding path bench.py runs at N > 1:
+shard ranges, the chunked digest gather to rank 0 (sharded.PipelinedGather, async collectives),
+the checksum-of-checksums verification, the one-shot gather and the combine-joined stream CRC, and
+bench.py's own rank spawner. The per-shard compute is the GPU kernel on a real run; here each rank
+uses the CPU oracle as the stand-in producer of its chunk's digests, so these tests check the
+distributed plumbing, not the kernel (the kernel's parity is tests/test_gpu_*.py)."""
 import os
 import socket
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -11,6 +15,8 @@ import torch
 import torch.multiprocessing as mp
 
 import oracle
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _free_port():
@@ -67,6 +73,76 @@ def test_gloo_world2_shard_gather_and_stream(n):
     assert len(streams) == 2 and all(s[2] == full for s in streams)
 
 
+def _pipe_worker(rank, world, port, n_local, L, chunks, q, corrupt):
+    """bench.py's N > 1 step: each rank produces its shard's digests chunk by chunk; every chunk is
+    gathered to rank 0 asynchronously while the next one is produced; then verify_gather."""
+    import torch.distributed as dist
+
+    from annety_amd import sharded
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        arena = oracle.lcg_bytes(n_local * L, 1000 + rank)  # each rank's own shard (weak scaling)
+        out = torch.zeros(n_local, dtype=torch.int32)
+        pipe = sharded.PipelinedGather(n_local, chunks, dst=0)
+
+        def produce(lo, hi):
+            d = oracle.batch_fixed(arena[lo * L:hi * L], hi - lo, L)
+            out[lo:hi] = torch.from_numpy(d.view(np.int32).copy())
+            return out[lo:hi]
+
+        handles = pipe.run(produce)
+        sharded.PipelinedGather.wait(handles)
+        if corrupt and rank == 0:
+            pipe.recv[1, 3] ^= 1
+        ok = sharded.verify_gather(pipe.recv, out)
+        q.put(("ok", rank, ok, len(pipe.bounds)))
+        if rank == 0:
+            q.put(("recv", pipe.recv.numpy().view(np.uint32).tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("corrupt", [False, True])
+def test_gloo_world2_pipelined_gather(corrupt):
+    n_local, L, chunks = 1000, 128, 7
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_pipe_worker, args=(r, 2, port, n_local, L, chunks, q, corrupt)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    msgs = [q.get(timeout=5) for _ in range(3)]
+    oks = [m for m in msgs if m[0] == "ok"]
+    assert all(m[2] == (not corrupt) for m in oks) and all(m[3] == chunks for m in oks)
+    recv = [m for m in msgs if m[0] == "recv"][0][1]
+    for r in range(2):
+        want = oracle.batch_fixed(oracle.lcg_bytes(n_local * L, 1000 + r), n_local, L).tolist()
+        if corrupt and r == 1:
+            want[3] ^= 1
+        assert recv[r] == want
+
+
+def test_bench_spawns_ranks(tmp_path):
+    """bench.py --gpus N without a launcher starts N ranks with the torchrun environment."""
+    sys.path.insert(0, ROOT)
+    import bench
+
+    script = tmp_path / "rank.py"
+    script.write_text("import os\nprint(os.environ['RANK'], os.environ['LOCAL_RANK'], os.environ['WORLD_SIZE'], "
+                      "os.environ['MASTER_ADDR'])\n")
+    out = subprocess.run([sys.executable, "-c", f"import sys; sys.path.insert(0, {ROOT!r}); import bench; "
+                          f"sys.exit(bench.spawn(3, [{str(script)!r}]))"], capture_output=True, text=True, timeout=60)
+    assert out.returncode == 0
+    assert out.stdout.split() == ["0", "0", "3", "127.0.0.1"]  # rank 0's stdout only
+    assert bench.spawn(2, ["-c", "import sys; sys.exit(3)"]) == 3
+
+
 def test_shard_range_covers():
     from annety_amd import sharded
 
@@ -76,3 +152,5 @@ def test_shard_range_covers():
             assert rs[0][0] == 0 and rs[-1][1] == n
             assert all(a[1] == b[0] for a, b in zip(rs, rs[1:]))
             assert max(h - l for l, h in rs) - min(h - l for l, h in rs) <= 1
+    assert sharded.chunk_bounds(10, 3) == [(0, 3), (3, 6), (6, 10)]
+    assert sharded.chunk_bounds(2, 8) == [(0, 1), (1, 2)]
