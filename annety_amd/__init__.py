@@ -20,6 +20,7 @@ from .crc32c import (  # noqa: F401
     crc32_combine,
     crc32_update_batch,
     crc32_update_batch_var,
+    PinnedHostBuffer,
     StreamingCrc,
     digests_to_numpy,
     tables,
@@ -34,6 +35,7 @@ __all__ = [
     "crc32_update_batch",
     "crc32_update_batch_var",
     "StreamingCrc",
+    "PinnedHostBuffer",
     "crc32_batch_host",
     "crc32_combine",
     "digests_to_numpy",

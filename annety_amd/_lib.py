@@ -34,6 +34,8 @@ SIGNATURES = [
     ("annety_crc32_batch_var_arena", ctypes.c_int, [_vp, _c_size, _vp, _vp, _c_size, _vp, _vp]),
     ("annety_crc32_update_batch_var_arena", ctypes.c_int, [_vp, _vp, _c_size, _vp, _vp, _c_size, _vp]),
     ("annety_crc32_batch_fixed_host", ctypes.c_int, [_vp, _c_size, _c_size, _c_size, _vp]),
+    ("annety_crc_host_register", ctypes.c_int, [_vp, _c_size]),
+    ("annety_crc_host_unregister", ctypes.c_int, [_vp]),
     ("annety_crc_shard_plan", ctypes.c_int, [_c_size, ctypes.c_int, _vp, _vp]),
     ("annety_crc_group_create", ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(_vp)]),
     ("annety_crc_group_destroy", ctypes.c_int, [_vp]),
@@ -44,6 +46,8 @@ SIGNATURES = [
                                         ctypes.POINTER(_c_size), ctypes.POINTER(_c_size)]),
     ("annety_lhc_verify_batch", ctypes.c_int, [_vp, _vp, _vp, _c_size, _vp, _vp, _vp]),
     ("annety_lhc_verify_stream", ctypes.c_int, [_vp, _c_size, _vp, _vp, _c_size, _vp, _vp, _vp]),
+    ("annety_lhc_verify_host", ctypes.c_int, [_vp, _c_size, ctypes.c_int, ctypes.c_int64, _vp, _vp, _vp, _c_size,
+                                              ctypes.POINTER(_c_size), ctypes.POINTER(_c_size)]),
     ("annety_lhc_encode_plan", ctypes.c_int, [_vp, _c_size, ctypes.c_int, ctypes.c_int64, _vp, _vp,
                                               ctypes.POINTER(_u64)]),
     ("annety_lhc_encode_batch", ctypes.c_int, [_vp, _vp, _vp, _c_size, ctypes.c_int, ctypes.c_int64, _vp, _vp,

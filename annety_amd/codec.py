@@ -142,6 +142,22 @@ class LengthHeaderCodec:
             ok = np.zeros(0, dtype=np.uint8)
         return recv_result(self.length_type, off, ln, used, invalid, ok)
 
+    def decode_host(self, stream: BytesLike, max_frames: int | None = None) -> DecodeResult:
+        """Codec::recv over a host receive buffer in one call (annety_lhc_verify_host): the header walk
+        overlaps the stream's copy to the current device, the CRCs are checked there."""
+        addr, size, keep = _host_view(stream)
+        cap = size // (self.length_type + 4) + 1 if max_frames is None else int(max_frames)
+        off = np.zeros(cap, dtype=np.uint64)
+        ln = np.zeros(cap, dtype=np.uint32)
+        ok = np.zeros(cap, dtype=np.uint8)
+        k, used = ctypes.c_size_t(), ctypes.c_size_t()
+        st = _lib.get().annety_lhc_verify_host(addr or None, size, self.length_type, self.max_payload, off.ctypes.data,
+                                               ln.ctypes.data, ok.ctypes.data, cap, ctypes.byref(k), ctypes.byref(used))
+        if st < 0:
+            _lib.check(st, "annety_lhc_verify_host")
+        n = k.value
+        return recv_result(self.length_type, off[:n], ln[:n], int(used.value), st == 1, ok[:n])
+
     # ---------------- encode ----------------
     def plan(self, lengths: np.ndarray):
         """annety_lhc_encode_plan: (frame_off u64[n], rt i8[n], total bytes)."""

@@ -252,6 +252,26 @@ def crc32_batch_host(buf: BytesLike, n: int, length: int, stride: Optional[int] 
     return out
 
 
+class PinnedHostBuffer:
+    """A host buffer registered with the device runtime (annety_crc_host_register), e.g. the arena a
+    NetBuffer reads sockets into: host batches over it are copied to the device in place."""
+
+    def __init__(self, nbytes: int):
+        self.array = np.empty(nbytes, dtype=np.uint8)
+        _lib.check(_lib.get().annety_crc_host_register(self.array.ctypes.data, nbytes), "annety_crc_host_register")
+
+    def close(self):
+        if self.array is not None:
+            _lib.get().annety_crc_host_unregister(self.array.ctypes.data)
+            self.array = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
 def digests_to_numpy(out) -> np.ndarray:
     """int32 device tensor of digests -> uint32 numpy array."""
     return out.detach().cpu().numpy().view(np.uint32)

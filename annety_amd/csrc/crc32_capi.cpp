@@ -8,8 +8,11 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
+#include <condition_variable>
 #include <cstring>
+#include <functional>
 #include <mutex>
+#include <thread>
 #include <vector>
 
 #include "crc32_kernels.h"
@@ -31,6 +34,126 @@ int hip_fail(hipError_t e) {
     hipError_t e_ = (expr);                    \
     if (e_ != hipSuccess) return hip_fail(e_); \
   } while (0)
+
+// ---------------- host worker pool (staging packs) ----------------
+// Pageable -> pinned packing is a host memcpy; one thread moves ~10-20 GB/s, below PCIe Gen5 x16, so the
+// pack is split over a small persistent pool (ANNETY_CRC_PACK_THREADS, default min(8, cores)).
+class PackPool {
+ public:
+  static PackPool& get() {
+    static PackPool pool;
+    return pool;
+  }
+  int threads() const { return (int)workers_.size() + 1; }
+  // Runs fn(i) for i in [0, n) on the pool and the calling thread; returns when all are done.
+  template <class F>
+  void run(size_t n, F&& fn) {
+    if (n == 0) return;
+    if (workers_.empty() || n == 1) {
+      for (size_t i = 0; i < n; i++) fn(i);
+      return;
+    }
+    std::unique_lock<std::mutex> one(run_mu_);  // one parallel region at a time
+    std::function<void(size_t)> f = fn;
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      job_ = &f;
+      next_ = 0;
+      total_ = n;
+      left_ = n;
+      gen_++;
+    }
+    cv_.notify_all();
+    work();
+    std::unique_lock<std::mutex> lk(mu_);
+    done_cv_.wait(lk, [&] { return left_ == 0; });
+    job_ = nullptr;
+  }
+
+ private:
+  PackPool() {
+    int t = (int)std::min<unsigned>(8, std::max<unsigned>(1, std::thread::hardware_concurrency()));
+    if (const char* e = std::getenv("ANNETY_CRC_PACK_THREADS")) t = std::max(1, std::min(64, std::atoi(e)));
+    for (int i = 1; i < t; i++) workers_.emplace_back([this] { loop(); });
+  }
+  ~PackPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& w : workers_) w.join();
+  }
+  void work() {
+    for (;;) {
+      size_t i;
+      std::function<void(size_t)>* f;
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (!job_ || next_ >= total_) return;
+        i = next_++;
+        f = job_;
+      }
+      (*f)(i);
+      std::lock_guard<std::mutex> lk(mu_);
+      if (--left_ == 0) done_cv_.notify_all();
+    }
+  }
+  void loop() {
+    uint64_t seen = 0;
+    for (;;) {
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        if (stop_) return;
+        seen = gen_;
+      }
+      work();
+    }
+  }
+  std::vector<std::thread> workers_;
+  std::mutex mu_, run_mu_;
+  std::condition_variable cv_, done_cv_;
+  std::function<void(size_t)>* job_ = nullptr;
+  size_t next_ = 0, total_ = 0, left_ = 0;
+  uint64_t gen_ = 0;
+  bool stop_ = false;
+};
+
+// dst[i*dstride, +len) = src[i*sstride, +len) for i < cnt, in parallel pieces of >= 1 MiB.
+void parallel_pack(char* dst, size_t dstride, const char* src, size_t sstride, size_t cnt, size_t len) {
+  if (dstride == sstride && dstride == len) {  // one contiguous block
+    const size_t bytes = cnt * len, piece = std::max<size_t>(1 << 20, bytes / (4 * PackPool::get().threads()) + 1);
+    PackPool::get().run((bytes + piece - 1) / piece, [&](size_t i) {
+      const size_t lo = i * piece, hi = std::min(bytes, lo + piece);
+      std::memcpy(dst + lo, src + lo, hi - lo);
+    });
+    return;
+  }
+  const size_t per = std::max<size_t>(1, (1 << 20) / std::max<size_t>(len, 1));
+  PackPool::get().run((cnt + per - 1) / per, [&](size_t i) {
+    const size_t lo = i * per, hi = std::min(cnt, lo + per);
+    for (size_t k = lo; k < hi; k++) std::memcpy(dst + k * dstride, src + k * sstride, len);
+  });
+}
+
+// true if [p, p + bytes) is pinned (hipHostMalloc'd or hipHostRegister'ed) host memory, so the DMA
+// engines can read it in place.
+bool host_pinned(const void* p, size_t bytes) {
+  hipPointerAttribute_t at{};
+  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  if (at.type != hipMemoryTypeHost) return false;
+  if (bytes <= 1) return true;
+  hipPointerAttribute_t end{};
+  if (hipPointerGetAttributes(&end, static_cast<const char*>(p) + bytes - 1) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  return end.type == hipMemoryTypeHost;
+}
 
 // ---------------- host-built LDS images ----------------
 constexpr int kGroups[] = {1, 2, 4, 8, 16, 32};
@@ -153,6 +276,11 @@ struct Staging {
   hipStream_t stream[2] = {nullptr, nullptr};
   hipEvent_t done[2] = {nullptr, nullptr};
   size_t bytes = 0, outs = 0;
+  // frame path (annety_lhc_verify_host): the received stream and its per-frame metadata on the device
+  char* d_stream = nullptr;
+  size_t stream_cap = 0;
+  char* d_meta = nullptr;  // off (8 B) + len (4 B) + digest (4 B) + ok (1 B) per frame
+  size_t meta_cap = 0;     // frames
 };
 
 struct DeviceCtx {
@@ -384,6 +512,7 @@ uint64_t split_segment(size_t n, uint64_t len, int cus) {
   if (len < 2 * seg) return 0;
   const uint64_t S = (len + seg - 1) / seg;
   if ((uint64_t)n * S > 0xFFFFFFFFull) return 0;  // descriptor indices are 32-bit
+  if (mode == 1) return seg;                        // forced (tests, tuning)
   // auto: whole payloads leave 32-lane groups idle (or a long tail) when there are fewer than two
   // payloads per group; with more, whole payloads measured slightly faster.
   const size_t groups_chip = (size_t)cus * fixed_kernel_block() / 32;
@@ -499,6 +628,8 @@ int annety_crc_shutdown(void) {
       if (c.stg.d_buf[i]) (void)hipFree(c.stg.d_buf[i]);
       if (c.stg.d_out[i]) (void)hipFree(c.stg.d_out[i]);
     }
+    if (c.stg.d_stream) (void)hipFree(c.stg.d_stream);
+    if (c.stg.d_meta) (void)hipFree(c.stg.d_meta);
     c.stg = Staging{};
     {
       std::lock_guard<std::mutex> pl(c.pow_mu);
@@ -577,6 +708,7 @@ int annety_crc32_batch_fixed(const void* d_base, size_t n, size_t len, size_t st
   if (const uint64_t seg = split_segment(n, len, c->cus)) return run_split(*c, d_base, n, len, stride, seg, d_out, s);
   if (len > 0xFFFFFFFFull) return ANNETY_CRC_EINVAL;  // whole-payload kernels take 32-bit lengths
   if (fixed_fast_ok(d_base, len, stride)) return run_fixed(*c, d_base, n, len, stride, d_out, false, s);
+  if (n > 0xFFFFFFFFull) return ANNETY_CRC_EINVAL;  // the general kernel's task descriptors hold 32-bit indices
   const uint64_t lines = (len + 255) / 128;
   return run_var(*c, d_base, n, stride, (uint32_t)len, pick_group(lines, n, c->cus), nullptr, nullptr, d_out, s);
 }
@@ -622,6 +754,7 @@ int annety_crc32_update_batch_fixed(uint32_t* d_state, const void* d_base, size_
   if (rc) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (fixed_fast_ok(d_base, len, stride)) return run_fixed(*c, d_base, n, len, stride, d_state, true, s);
+  if (n > 0xFFFFFFFFull) return ANNETY_CRC_EINVAL;  // 32-bit task indices in the general kernel
   const uint64_t lines = (len + 255) / 128;  // odd shapes: the general kernel in update mode
   return run_var(*c, d_base, n, stride, (uint32_t)len, pick_group(lines, n, c->cus), nullptr, nullptr, d_state, s,
                  true);
@@ -636,6 +769,29 @@ int annety_crc32_update_batch_var(uint32_t* d_state, const void* d_base, const u
   int rc = current_ctx(&c);
   if (rc) return rc;
   return run_var_sorted(*c, d_base, n, d_off, d_len, d_state, static_cast<hipStream_t>(stream), true);
+}
+
+// Staging ring of the current device's context, allocated for at least `need` bytes per slot.
+static int ensure_ring(Staging& st, size_t need, size_t outs) {
+  if (st.bytes >= need && st.outs >= outs) return ANNETY_CRC_OK;
+  for (int i = 0; i < 2; i++) {
+    if (st.h_pinned[i]) (void)hipHostFree(st.h_pinned[i]);
+    if (st.d_buf[i]) (void)hipFree(st.d_buf[i]);
+    if (st.d_out[i]) (void)hipFree(st.d_out[i]);
+    if (st.h_out[i]) (void)hipHostFree(st.h_out[i]);
+    st.h_pinned[i] = st.d_buf[i] = nullptr;
+    st.d_out[i] = st.h_out[i] = nullptr;
+    st.bytes = st.outs = 0;
+    HIP_TRY(hipHostMalloc(&st.h_pinned[i], need, hipHostMallocDefault));
+    HIP_TRY(hipMalloc(&st.d_buf[i], need));
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&st.d_out[i]), outs * 4));
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&st.h_out[i]), outs * 4, hipHostMallocDefault));
+    if (!st.stream[i]) HIP_TRY(hipStreamCreateWithFlags(&st.stream[i], hipStreamNonBlocking));
+    if (!st.done[i]) HIP_TRY(hipEventCreateWithFlags(&st.done[i], hipEventDisableTiming));
+  }
+  st.bytes = need;
+  st.outs = outs;
+  return ANNETY_CRC_OK;
 }
 
 int annety_crc32_batch_fixed_host(const void* h_base, size_t n, size_t len, size_t stride, uint32_t* h_out) {
@@ -655,55 +811,58 @@ int annety_crc32_batch_fixed_host(const void* h_base, size_t n, size_t len, size
   size_t per = std::max<size_t>(1, (64u << 20) / plen);
   per = std::min(per, n);
   const size_t need = per * plen;
-  if (st.bytes < need || st.outs < per) {
-    for (int i = 0; i < 2; i++) {
-      if (st.h_pinned[i]) (void)hipHostFree(st.h_pinned[i]);
-      if (st.d_buf[i]) (void)hipFree(st.d_buf[i]);
-      if (st.d_out[i]) (void)hipFree(st.d_out[i]);
-      if (st.h_out[i]) (void)hipHostFree(st.h_out[i]);
-      st.h_pinned[i] = st.d_buf[i] = nullptr;
-      st.d_out[i] = st.h_out[i] = nullptr;
-      st.bytes = st.outs = 0;
-      HIP_TRY(hipHostMalloc(&st.h_pinned[i], need, hipHostMallocDefault));
-      HIP_TRY(hipMalloc(&st.d_buf[i], need));
-      HIP_TRY(hipMalloc(reinterpret_cast<void**>(&st.d_out[i]), per * 4));
-      HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&st.h_out[i]), per * 4, hipHostMallocDefault));
-      if (!st.stream[i]) HIP_TRY(hipStreamCreateWithFlags(&st.stream[i], hipStreamNonBlocking));
-      if (!st.done[i]) HIP_TRY(hipEventCreateWithFlags(&st.done[i], hipEventDisableTiming));
-    }
-    st.bytes = need;
-    st.outs = per;
-  }
+  if ((rc = ensure_ring(st, need, per))) return rc;
   const char* src = static_cast<const char*>(h_base);
+  // caller memory that is already pinned (hipHostRegister'ed NetBuffer arenas) is DMA'd in place when
+  // the payloads are packed 16-byte multiples; otherwise it is packed into the pinned ring in parallel
+  const bool direct = stride == plen && host_pinned(h_base, (n - 1) * stride + len);
   size_t pending_lo[2] = {0, 0}, pending_n[2] = {0, 0};
+  auto drain = [&](int i) -> int {  // wait for slot i's batch and copy its digests out
+    if (!pending_n[i]) return ANNETY_CRC_OK;
+    const hipError_t e = hipEventSynchronize(st.done[i]);
+    if (e == hipSuccess) std::memcpy(h_out + pending_lo[i], st.h_out[i], pending_n[i] * 4);
+    pending_n[i] = 0;
+    return e == hipSuccess ? ANNETY_CRC_OK : hip_fail(e);
+  };
+  auto fail = [&](int status) {  // leave no copy in flight on the shared staging buffers
+    (void)hipStreamSynchronize(st.stream[0]);
+    (void)hipStreamSynchronize(st.stream[1]);
+    return status;
+  };
   int slot = 0;
   for (size_t lo = 0; lo < n; lo += per, slot ^= 1) {
     const size_t cnt = std::min(per, n - lo);
-    if (pending_n[slot]) {  // drain the previous use of this slot
-      HIP_TRY(hipEventSynchronize(st.done[slot]));
-      std::memcpy(h_out + pending_lo[slot], st.h_out[slot], pending_n[slot] * 4);
-      pending_n[slot] = 0;
+    if ((rc = drain(slot))) return fail(rc);  // the previous use of this slot
+    const char* from = src + lo * stride;
+    if (!direct) {  // pack payloads into the pinned slot (the host side of a NetBuffer -> device hand-off)
+      char* dst = static_cast<char*>(st.h_pinned[slot]);
+      parallel_pack(dst, plen, from, stride, cnt, len);
+      from = dst;
     }
-    // pack payloads into the pinned slot (the host side of a NetBuffer -> device hand-off)
-    char* dst = static_cast<char*>(st.h_pinned[slot]);
-    if (stride == plen) {
-      std::memcpy(dst, src + lo * stride, cnt * plen - (plen - len));
-    } else {
-      for (size_t i = 0; i < cnt; i++) std::memcpy(dst + i * plen, src + (lo + i) * stride, len);
-    }
-    HIP_TRY(hipMemcpyAsync(st.d_buf[slot], dst, cnt * plen, hipMemcpyHostToDevice, st.stream[slot]));
+    hipError_t e = hipMemcpyAsync(st.d_buf[slot], from, cnt * plen - (plen - len), hipMemcpyHostToDevice, st.stream[slot]);
+    if (e != hipSuccess) return fail(hip_fail(e));
     rc = annety_crc32_batch_fixed(st.d_buf[slot], cnt, len, plen, st.d_out[slot], st.stream[slot]);
-    if (rc) return rc;
-    HIP_TRY(hipMemcpyAsync(st.h_out[slot], st.d_out[slot], cnt * 4, hipMemcpyDeviceToHost, st.stream[slot]));
-    HIP_TRY(hipEventRecord(st.done[slot], st.stream[slot]));
+    if (rc) return fail(rc);
+    e = hipMemcpyAsync(st.h_out[slot], st.d_out[slot], cnt * 4, hipMemcpyDeviceToHost, st.stream[slot]);
+    if (e == hipSuccess) e = hipEventRecord(st.done[slot], st.stream[slot]);
+    if (e != hipSuccess) return fail(hip_fail(e));
     pending_lo[slot] = lo;
     pending_n[slot] = cnt;
   }
   for (int i = 0; i < 2; i++)
-    if (pending_n[i]) {
-      HIP_TRY(hipEventSynchronize(st.done[i]));
-      std::memcpy(h_out + pending_lo[i], st.h_out[i], pending_n[i] * 4);
-    }
+    if ((rc = drain(i))) return fail(rc);
+  return ANNETY_CRC_OK;
+}
+
+int annety_crc_host_register(void* h_ptr, size_t bytes) {
+  if (!h_ptr || !bytes) return ANNETY_CRC_EINVAL;
+  HIP_TRY(hipHostRegister(h_ptr, bytes, hipHostRegisterDefault));
+  return ANNETY_CRC_OK;
+}
+
+int annety_crc_host_unregister(void* h_ptr) {
+  if (!h_ptr) return ANNETY_CRC_EINVAL;
+  HIP_TRY(hipHostUnregister(h_ptr));
   return ANNETY_CRC_OK;
 }
 
@@ -822,6 +981,103 @@ int annety_lhc_encode_batch(const void* d_src, const uint64_t* d_src_off, const 
   hipError_t e = hipFreeAsync(dig, s);
   if (rc == ANNETY_CRC_OK && e != hipSuccess) rc = hip_fail(e);
   return rc;
+}
+
+// Codec::recv over a host receive buffer (include/codec/Codec.h:52-76 + LengthHeaderCodec::decode :71-137):
+// the header walk runs on a helper thread while the stream is copied to the device through the pinned
+// ring (or straight from pinned caller memory); then every complete frame is verified on the device by
+// the arena path over the stream and the verdicts come back.
+int annety_lhc_verify_host(const void* h_stream, size_t size, int length_type, int64_t max_payload,
+                           uint64_t* h_payload_off, uint32_t* h_payload_len, uint8_t* h_ok, size_t max_frames,
+                           size_t* n_frames, size_t* consumed) {
+  if (!n_frames || !consumed || !lhc_type_ok(length_type) || (!h_stream && size) ||
+      (max_frames && (!h_payload_off || !h_payload_len || !h_ok)))
+    return ANNETY_CRC_EINVAL;
+  *n_frames = *consumed = 0;
+  if (size == 0 || max_frames == 0)
+    return annety_lhc_parse(h_stream, size, length_type, max_payload, h_payload_off, h_payload_len, max_frames,
+                            n_frames, consumed);
+  DeviceCtx* c = nullptr;
+  int rc = current_ctx(&c);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(c->stg_mu);
+  Staging& st = c->stg;
+  if ((rc = ensure_ring(st, std::max<size_t>(st.bytes, 64u << 20), std::max<size_t>(st.outs, 1)))) return rc;
+  if (st.stream_cap < size) {
+    if (st.d_stream) (void)hipFree(st.d_stream);
+    st.d_stream = nullptr;
+    st.stream_cap = 0;
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&st.d_stream), size));
+    st.stream_cap = size;
+  }
+  hipStream_t s = st.stream[0];
+  // walk the headers while the bytes go up
+  int prc = 0;
+  std::thread walker([&] {
+    prc = annety_lhc_parse(h_stream, size, length_type, max_payload, h_payload_off, h_payload_len, max_frames, n_frames,
+                           consumed);
+  });
+  auto fail = [&](int status) {
+    walker.join();
+    (void)hipStreamSynchronize(st.stream[0]);
+    (void)hipStreamSynchronize(st.stream[1]);
+    return status;
+  };
+  const char* src = static_cast<const char*>(h_stream);
+  if (host_pinned(h_stream, size)) {
+    const hipError_t e = hipMemcpyAsync(st.d_stream, src, size, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) return fail(hip_fail(e));
+  } else {
+    const size_t piece = st.bytes;
+    bool busy[2] = {false, false};
+    int slot = 0;
+    for (size_t lo = 0; lo < size; lo += piece, slot ^= 1) {
+      const size_t cnt = std::min(piece, size - lo);
+      if (busy[slot]) {
+        const hipError_t e = hipEventSynchronize(st.done[slot]);
+        if (e != hipSuccess) return fail(hip_fail(e));
+      }
+      parallel_pack(static_cast<char*>(st.h_pinned[slot]), cnt, src + lo, cnt, 1, cnt);
+      hipError_t e = hipMemcpyAsync(st.d_stream + lo, st.h_pinned[slot], cnt, hipMemcpyHostToDevice, s);
+      if (e == hipSuccess) e = hipEventRecord(st.done[slot], s);
+      if (e != hipSuccess) return fail(hip_fail(e));
+      busy[slot] = true;
+    }
+  }
+  walker.join();
+  if (prc < 0) {
+    (void)hipStreamSynchronize(s);
+    return prc;
+  }
+  const size_t k = *n_frames;
+  if (k) {
+    if (st.meta_cap < k) {
+      if (st.d_meta) (void)hipFree(st.d_meta);
+      st.d_meta = nullptr;
+      st.meta_cap = 0;
+      HIP_TRY(hipMalloc(reinterpret_cast<void**>(&st.d_meta), k * 17));
+      st.meta_cap = k;
+    }
+    uint64_t* d_off = reinterpret_cast<uint64_t*>(st.d_meta);
+    uint32_t* d_len = reinterpret_cast<uint32_t*>(st.d_meta + k * 8);
+    uint32_t* d_dig = d_len + k;
+    uint8_t* d_ok = reinterpret_cast<uint8_t*>(d_dig + k);
+    hipError_t e = hipMemcpyAsync(d_off, h_payload_off, k * 8, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_len, h_payload_len, k * 4, hipMemcpyHostToDevice, s);
+    if (e != hipSuccess) {
+      (void)hipStreamSynchronize(s);
+      return hip_fail(e);
+    }
+    rc = run_arena(*c, st.d_stream, *consumed, d_off, d_len, k, d_dig, s, false);
+    if (rc == ANNETY_CRC_OK) {
+      e = launch_lhc_compare(st.d_stream, d_off, d_len, k, d_dig, d_ok, s);
+      if (e == hipSuccess) e = hipMemcpyAsync(h_ok, d_ok, k, hipMemcpyDeviceToHost, s);
+      if (e != hipSuccess) rc = hip_fail(e);
+    }
+  }
+  const hipError_t e = hipStreamSynchronize(s);
+  if (rc == ANNETY_CRC_OK && e != hipSuccess) rc = hip_fail(e);
+  return rc ? rc : prc;
 }
 
 }  // extern "C"

@@ -94,9 +94,14 @@ int annety_crc32_batch_var_arena(const void* d_arena, size_t arena_bytes, const 
 int annety_crc32_update_batch_var_arena(uint32_t* d_state, const void* d_arena, size_t arena_bytes,
                                         const uint64_t* d_off, const uint32_t* d_len, size_t n, void* stream);
 
-/* ---- host-memory batch (payloads off a NetBuffer/socket): staged through pinned buffers, H2D ->
- * kernel -> D2H, pipelined on two streams. Synchronous. ---- */
+/* ---- host-memory batch (payloads off a NetBuffer/socket): staged through pinned buffers (packed by a
+ * small host thread pool, ANNETY_CRC_PACK_THREADS), H2D -> kernel -> D2H, pipelined on two streams.
+ * Synchronous. ---- */
 int annety_crc32_batch_fixed_host(const void* h_base, size_t n, size_t len, size_t stride, uint32_t* h_out);
+/* Pin (hipHostRegister) / unpin a long-lived host buffer, e.g. a NetBuffer arena: host batches whose
+ * payloads lie in pinned memory are copied to the device in place, without the staging pack. */
+int annety_crc_host_register(void* h_ptr, size_t bytes);
+int annety_crc_host_unregister(void* h_ptr);
 
 /* ---- device groups: one process, several gfx950 devices ----
  * A group is an RCCL communicator over `devices` (ncclCommInitAll, single process) plus a compute and a
@@ -148,6 +153,15 @@ int annety_lhc_verify_batch(const void* d_stream, const uint64_t* d_payload_off,
 int annety_lhc_verify_stream(const void* d_stream, size_t stream_bytes, const uint64_t* d_payload_off,
                              const uint32_t* d_payload_len, size_t n, uint8_t* d_ok, uint32_t* d_digest,
                              void* stream);
+/* Codec::recv over a host receive buffer (include/codec/Codec.h:52-76, the NetBuffer of
+ * src/TcpConnection.cc:438-461): the header walk of annety_lhc_parse runs on a helper thread while the
+ * stream is copied to the current device (through the pinned staging ring, or in place when h_stream is
+ * pinned), then every complete frame's CRC is verified on the device (arena path over the stream).
+ * Outputs as annety_lhc_parse plus h_ok[i] = 1 if frame i's trailer matches. Returns 0, 1 (the walk
+ * stopped on an invalid length: decode's -1) or a negative error. Synchronous. */
+int annety_lhc_verify_host(const void* h_stream, size_t size, int length_type, int64_t max_payload,
+                           uint64_t* h_payload_off, uint32_t* h_payload_len, uint8_t* h_ok, size_t max_frames,
+                           size_t* n_frames, size_t* consumed);
 /* Host plan for a batch of LengthHeaderCodec::encode calls (:169-176): h_rt[i] (optional) = 1, or 0 for
  * an empty payload, or -1 for len > max_payload (max_payload > 0); h_frame_off[i] = where frame i starts
  * when the frames of accepted payloads are packed back to back (rejected ones take no bytes);

@@ -114,6 +114,50 @@ def test_gpu_decode_matches_reference(golden, gpu):
 
 
 @pytest.mark.gpu
+def test_gpu_decode_host_matches_reference(golden, gpu):
+    """annety_lhc_verify_host (walk overlapped with the upload, verify on the device) = Codec::recv."""
+    for c in golden("lhc.json")["decode"]:
+        codec = LengthHeaderCodec(c["T"], True, c["max_payload"])
+        r = codec.decode_host(bytes.fromhex(c["stream"]))
+        assert [[int(o), int(n)] for o, n in zip(r.payload_off, r.payload_len)] == c["frames"], c["name"]
+        assert (r.consumed, r.rt) == (c["consumed"], c["rt"]), c["name"]
+
+
+@pytest.mark.gpu
+def test_gpu_decode_host_large_stream(gpu):
+    """A 200 MiB frame stream (several staging pieces) through decode_host, pageable and pinned,
+    with corrupted frames: verdicts equal the oracle's on every frame."""
+    import annety_amd
+
+    rng = np.random.default_rng(9)
+    lens = np.minimum(65536, 64 * rng.zipf(1.3, 6000) + rng.integers(0, 64, 6000)).astype(np.int64)
+    body = oracle.lcg_bytes(int(lens.sum()), 31)
+    pieces, pos = [], 0
+    for L in lens.tolist():
+        rt, fr = oracle.lhc_encode(body[pos:pos + L], 4)
+        pieces.append(fr)
+        pos += L
+    stream = bytearray(b"".join(pieces))
+    reps = 200 * 2 ** 20 // len(stream) + 1
+    stream = bytearray(bytes(stream) * reps)
+    bad = rng.choice(len(lens) * reps, 25, replace=False)
+    starts = np.concatenate([[0], np.cumsum(np.tile(lens + 8, reps))[:-1]])
+    for b in bad:
+        stream[int(starts[b]) + 4] ^= 0x40  # flip a payload bit -> checksum mismatch
+    codec = LengthHeaderCodec(4)
+    want_ok = np.ones(len(starts), dtype=np.uint8)
+    want_ok[bad] = 0
+    r = codec.decode_host(bytes(stream))
+    assert np.array_equal(r.ok, want_ok)
+    assert r.rt == -1 and r.consumed == int(starts[np.sort(bad)[0]])
+    pinned = annety_amd.PinnedHostBuffer(len(stream))
+    pinned.array[:] = np.frombuffer(bytes(stream), dtype=np.uint8)
+    r2 = codec.decode_host(pinned.array)
+    assert np.array_equal(r2.ok, want_ok)
+    pinned.close()
+
+
+@pytest.mark.gpu
 def test_gpu_encode_matches_reference(golden, gpu):
     import torch
 
