@@ -10,6 +10,8 @@ Public surface:
   crc32_batch_host        host-memory batch, staged over PCIe  (annety_crc32_batch_fixed_host)
   crc32_combine           join two digests                     (annety_crc32_combine)
   LengthHeaderCodec       batched frame verify/build for annety's LengthHeaderCodec wire format
+  ProtobufCodecFrames     the same for ProtobufCodec's framing (T = 4, 10 B .. 64 MiB)
+  PinnedHostBuffer        host arena registered for in-place DMA (annety_crc_host_register)
   sharded                 multi-GPU batch sharding helpers (torch.distributed / RCCL)
 """
 from .crc32c import (  # noqa: F401
@@ -26,7 +28,7 @@ from .crc32c import (  # noqa: F401
     tables,
 )
 from ._lib import CrcError, lib_path  # noqa: F401
-from .codec import LengthHeaderCodec  # noqa: F401
+from .codec import LengthHeaderCodec, ProtobufCodecFrames  # noqa: F401
 
 __all__ = [
     "Crc32c",
@@ -41,6 +43,7 @@ __all__ = [
     "digests_to_numpy",
     "tables",
     "LengthHeaderCodec",
+    "ProtobufCodecFrames",
     "CrcError",
     "lib_path",
 ]

@@ -159,6 +159,11 @@ class LengthHeaderCodec:
         return recv_result(self.length_type, off[:n], ln[:n], int(used.value), st == 1, ok[:n])
 
     # ---------------- encode ----------------
+    def _encode_call(self, d_src, d_soff, d_len, n, frames, d_foff, sh):
+        return _lib.get().annety_lhc_encode_batch(_dev_ptr(d_src), _dev_ptr(d_soff), _dev_ptr(d_len), n,
+                                                  self.length_type, self.max_payload, _dev_ptr(frames),
+                                                  _dev_ptr(d_foff), sh), "annety_lhc_encode_batch"
+
     def plan(self, lengths: np.ndarray):
         """annety_lhc_encode_plan: (frame_off u64[n], rt i8[n], total bytes)."""
         ln = np.ascontiguousarray(lengths, dtype=np.uint32)
@@ -190,8 +195,60 @@ class LengthHeaderCodec:
             d_len = torch.from_numpy(lengths.view(np.int32)).to(dev)
             d_foff = torch.from_numpy(frame_off.view(np.int64)).to(dev)
             with _on_device(d_src, frames):
-                st = _lib.get().annety_lhc_encode_batch(_dev_ptr(d_src), _dev_ptr(d_soff), _dev_ptr(d_len), n,
-                                                        self.length_type, self.max_payload, _dev_ptr(frames),
-                                                        _dev_ptr(d_foff), _stream_handle(stream, frames))
-            _lib.check(st, "annety_lhc_encode_batch")
+                st, name = self._encode_call(d_src, d_soff, d_len, n, frames, d_foff, _stream_handle(stream, frames))
+            _lib.check(st, name)
         return EncodeResult(frames, frame_off, rt)
+
+
+class ProtobufCodecFrames(LengthHeaderCodec):
+    """Batched framing of annety's ProtobufCodec (include/protobuf/ProtobufCodec.h, checksum on): the
+    LengthHeaderCodec wire layout with a 4-byte length and the codec's fixed limits (decode: length field
+    in [10, 64 MiB], :149-156, :273-283; encode: payload of 6 .. 64 MiB bytes, :223-230). The CRC covers
+    the whole payload (nameLen + typeName + message bytes, :235-247); the message itself stays opaque
+    (parsing it is the caller's, with libprotobuf)."""
+
+    MIN_PAYLOAD = 10
+    MAX_PAYLOAD = 64 * 1024 * 1024
+
+    def __init__(self):
+        super().__init__(self.kLengthType32, True, self.MAX_PAYLOAD)
+
+    def parse(self, stream: BytesLike, max_frames: int | None = None):
+        addr, size, keep = _host_view(stream)
+        cap = size // 8 + 1 if max_frames is None else int(max_frames)
+        off = np.zeros(cap, dtype=np.uint64)
+        ln = np.zeros(cap, dtype=np.uint32)
+        k, used = ctypes.c_size_t(), ctypes.c_size_t()
+        st = _lib.get().annety_pbc_parse(addr or None, size, off.ctypes.data, ln.ctypes.data, cap, ctypes.byref(k),
+                                         ctypes.byref(used))
+        if st < 0:
+            _lib.check(st, "annety_pbc_parse")
+        return off[: k.value], ln[: k.value], int(used.value), st == 1
+
+    def decode_host(self, stream: BytesLike, max_frames: int | None = None) -> DecodeResult:
+        addr, size, keep = _host_view(stream)
+        cap = size // 8 + 1 if max_frames is None else int(max_frames)
+        off = np.zeros(cap, dtype=np.uint64)
+        ln = np.zeros(cap, dtype=np.uint32)
+        ok = np.zeros(cap, dtype=np.uint8)
+        k, used = ctypes.c_size_t(), ctypes.c_size_t()
+        st = _lib.get().annety_pbc_verify_host(addr or None, size, off.ctypes.data, ln.ctypes.data, ok.ctypes.data, cap,
+                                               ctypes.byref(k), ctypes.byref(used))
+        if st < 0:
+            _lib.check(st, "annety_pbc_verify_host")
+        n = k.value
+        return recv_result(self.length_type, off[:n], ln[:n], int(used.value), st == 1, ok[:n])
+
+    def plan(self, lengths: np.ndarray):
+        ln = np.ascontiguousarray(lengths, dtype=np.uint32)
+        off = np.zeros(ln.size, dtype=np.uint64)
+        rt = np.zeros(ln.size, dtype=np.int8)
+        total = ctypes.c_uint64()
+        st = _lib.get().annety_pbc_encode_plan(ln.ctypes.data, ln.size, off.ctypes.data, rt.ctypes.data,
+                                               ctypes.byref(total))
+        _lib.check(st, "annety_pbc_encode_plan")
+        return off, rt, int(total.value)
+
+    def _encode_call(self, d_src, d_soff, d_len, n, frames, d_foff, sh):
+        return _lib.get().annety_pbc_encode_batch(_dev_ptr(d_src), _dev_ptr(d_soff), _dev_ptr(d_len), n,
+                                                  _dev_ptr(frames), _dev_ptr(d_foff), sh), "annety_pbc_encode_batch"

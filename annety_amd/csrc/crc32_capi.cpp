@@ -871,13 +871,28 @@ static bool lhc_type_ok(int t) { return t == 1 || t == 2 || t == 4 || t == 8; }
 
 // include/codec/LengthHeaderCodec.h:71-137 without the CRC: signed big-endian length (peek_int*),
 // min_payload = checksum_length = 4, max_payload check, completeness check.
-int annety_lhc_parse(const void* h_stream, size_t size, int length_type, int64_t max_payload, uint64_t* payload_off,
-                     uint32_t* payload_len, size_t max_frames, size_t* n_frames, size_t* consumed) {
-  if (!n_frames || !consumed || !lhc_type_ok(length_type) || (!h_stream && size) ||
-      (max_frames && (!payload_off || !payload_len)))
+// Framing rules of annety's two CRC codecs (same wire layout [len T BE][payload][crc BE]):
+//   decode: length (payload + 4) outside [dec_min, dec_max] is invalid (decode -1); dec_max <= 0: no limit
+//   encode: payload length 0 -> rt 0; outside [enc_min, enc_max] -> rt -1; enc_max <= 0: no limit
+struct FrameRules {
+  int T;
+  int64_t dec_min, dec_max, enc_min, enc_max;
+};
+// LengthHeaderCodec (include/codec/LengthHeaderCodec.h): min_payload() = checksum_length() = 4 (:214-217),
+// max_payload checked only when > 0 (:102, :174), decode :71-137, encode :146-201.
+static FrameRules lhc_rules(int T, int64_t max_payload) { return {T, 4, max_payload, 1, max_payload}; }
+// ProtobufCodec (include/protobuf/ProtobufCodec.h): T = kLengthType32 (:260-263), min_payload() =
+// header_length() 4 + 2 + checksum_length() 4 = 10 (:279-283), max_payload() = 64 MiB unconditional
+// (:273-277); decode rejects length < 10 or > 64 MiB (:149-153), encode rejects payload < 10 - 4 = 6 or
+// > 64 MiB (:229-233).
+static constexpr FrameRules kPbcRules = {4, 10, 64ll << 20, 6, 64ll << 20};
+
+static int parse_frames(const FrameRules& r, const void* h_stream, size_t size, uint64_t* payload_off,
+                        uint32_t* payload_len, size_t max_frames, size_t* n_frames, size_t* consumed) {
+  if (!n_frames || !consumed || !lhc_type_ok(r.T) || (!h_stream && size) || (max_frames && (!payload_off || !payload_len)))
     return ANNETY_CRC_EINVAL;
   const unsigned char* p = static_cast<const unsigned char*>(h_stream);
-  const size_t T = (size_t)length_type;
+  const size_t T = (size_t)r.T;
   size_t pos = 0, k = 0;
   int rc = ANNETY_CRC_OK;
   while (k < max_frames && size - pos >= T) {
@@ -890,7 +905,7 @@ int annety_lhc_parse(const void* h_stream, size_t size, int length_type, int64_t
       case 4: length = (int32_t)u; break;
       default: length = (int64_t)u; break;
     }
-    if (length < 4 || (max_payload > 0 && length > max_payload)) {
+    if (length < r.dec_min || (r.dec_max > 0 && length > r.dec_max)) {
       rc = 1;  // decode returns -1: invalid length
       break;
     }
@@ -907,6 +922,19 @@ int annety_lhc_parse(const void* h_stream, size_t size, int length_type, int64_t
   *n_frames = k;
   *consumed = pos;
   return rc;
+}
+
+// include/codec/LengthHeaderCodec.h:71-137 without the CRC: signed big-endian length (peek_int*),
+// min_payload = checksum_length = 4, max_payload check, completeness check.
+int annety_lhc_parse(const void* h_stream, size_t size, int length_type, int64_t max_payload, uint64_t* payload_off,
+                     uint32_t* payload_len, size_t max_frames, size_t* n_frames, size_t* consumed) {
+  return parse_frames(lhc_rules(length_type, max_payload), h_stream, size, payload_off, payload_len, max_frames,
+                      n_frames, consumed);
+}
+
+int annety_pbc_parse(const void* h_stream, size_t size, uint64_t* payload_off, uint32_t* payload_len,
+                     size_t max_frames, size_t* n_frames, size_t* consumed) {
+  return parse_frames(kPbcRules, h_stream, size, payload_off, payload_len, max_frames, n_frames, consumed);
 }
 
 static int lhc_verify(const void* d_stream, size_t stream_bytes, bool arena, const uint64_t* d_payload_off,
@@ -943,30 +971,29 @@ int annety_lhc_verify_stream(const void* d_stream, size_t stream_bytes, const ui
   return lhc_verify(d_stream, stream_bytes, true, d_payload_off, d_payload_len, n, d_ok, d_digest, stream);
 }
 
-// LengthHeaderCodec::encode's per-payload decision (:169-176): rt 0 for an empty payload, -1 for
-// len > max_payload (max_payload > 0), else 1 with a frame of T + len + 4 bytes. Rejected payloads
+// encode()'s per-payload decision (LengthHeaderCodec :169-176, ProtobufCodec :225-233): rt 0 for an empty
+// payload, -1 outside [enc_min, enc_max], else 1 with a frame of T + len + 4 bytes. Rejected payloads
 // get zero bytes, so the frames of the accepted ones are packed back to back as consecutive encode
 // calls on one NetBuffer would leave them.
-int annety_lhc_encode_plan(const uint32_t* h_len, size_t n, int length_type, int64_t max_payload,
-                           uint64_t* h_frame_off, int8_t* h_rt, uint64_t* total) {
-  if (!lhc_type_ok(length_type) || !total || (n && (!h_len || !h_frame_off))) return ANNETY_CRC_EINVAL;
+static int encode_plan(const FrameRules& r, const uint32_t* h_len, size_t n, uint64_t* h_frame_off, int8_t* h_rt,
+                       uint64_t* total) {
+  if (!lhc_type_ok(r.T) || !total || (n && (!h_len || !h_frame_off))) return ANNETY_CRC_EINVAL;
   uint64_t pos = 0;
   for (size_t i = 0; i < n; i++) {
-    const uint32_t L = h_len[i];
-    const int8_t rt = L == 0 ? 0 : (max_payload > 0 && (int64_t)L > max_payload) ? -1 : 1;
+    const int64_t L = h_len[i];
+    const int8_t rt = L == 0 ? 0 : (L < r.enc_min || (r.enc_max > 0 && L > r.enc_max)) ? -1 : 1;
     if (h_rt) h_rt[i] = rt;
     h_frame_off[i] = pos;
-    if (rt == 1) pos += (uint64_t)length_type + L + 4;
+    if (rt == 1) pos += (uint64_t)r.T + (uint64_t)L + 4;
   }
   *total = pos;
   return ANNETY_CRC_OK;
 }
 
-int annety_lhc_encode_batch(const void* d_src, const uint64_t* d_src_off, const uint32_t* d_len, size_t n,
-                            int length_type, int64_t max_payload, void* d_dst, const uint64_t* d_frame_off,
-                            void* stream) {
+static int encode_batch(const FrameRules& r, const void* d_src, const uint64_t* d_src_off, const uint32_t* d_len,
+                        size_t n, void* d_dst, const uint64_t* d_frame_off, void* stream) {
   if (n == 0) return ANNETY_CRC_OK;
-  if (!lhc_type_ok(length_type) || !d_src || !d_src_off || !d_len || !d_dst || !d_frame_off) return ANNETY_CRC_EINVAL;
+  if (!lhc_type_ok(r.T) || !d_src || !d_src_off || !d_len || !d_dst || !d_frame_off) return ANNETY_CRC_EINVAL;
   DeviceCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
@@ -975,7 +1002,7 @@ int annety_lhc_encode_batch(const void* d_src, const uint64_t* d_src_off, const 
   HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&dig), n * sizeof(uint32_t), s));
   rc = annety_crc32_batch_var(d_src, d_src_off, d_len, n, dig, stream);
   if (rc == ANNETY_CRC_OK) {
-    hipError_t e = launch_lhc_encode(d_src, d_src_off, d_len, n, length_type, max_payload, d_dst, d_frame_off, dig, s);
+    hipError_t e = launch_lhc_encode(d_src, d_src_off, d_len, n, r.T, r.enc_min, r.enc_max, d_dst, d_frame_off, dig, s);
     if (e != hipSuccess) rc = hip_fail(e);
   }
   hipError_t e = hipFreeAsync(dig, s);
@@ -983,20 +1010,38 @@ int annety_lhc_encode_batch(const void* d_src, const uint64_t* d_src_off, const 
   return rc;
 }
 
+int annety_lhc_encode_plan(const uint32_t* h_len, size_t n, int length_type, int64_t max_payload,
+                           uint64_t* h_frame_off, int8_t* h_rt, uint64_t* total) {
+  return encode_plan(lhc_rules(length_type, max_payload), h_len, n, h_frame_off, h_rt, total);
+}
+
+int annety_lhc_encode_batch(const void* d_src, const uint64_t* d_src_off, const uint32_t* d_len, size_t n,
+                            int length_type, int64_t max_payload, void* d_dst, const uint64_t* d_frame_off,
+                            void* stream) {
+  return encode_batch(lhc_rules(length_type, max_payload), d_src, d_src_off, d_len, n, d_dst, d_frame_off, stream);
+}
+
+int annety_pbc_encode_plan(const uint32_t* h_len, size_t n, uint64_t* h_frame_off, int8_t* h_rt, uint64_t* total) {
+  return encode_plan(kPbcRules, h_len, n, h_frame_off, h_rt, total);
+}
+
+int annety_pbc_encode_batch(const void* d_src, const uint64_t* d_src_off, const uint32_t* d_len, size_t n,
+                            void* d_dst, const uint64_t* d_frame_off, void* stream) {
+  return encode_batch(kPbcRules, d_src, d_src_off, d_len, n, d_dst, d_frame_off, stream);
+}
+
 // Codec::recv over a host receive buffer (include/codec/Codec.h:52-76 + LengthHeaderCodec::decode :71-137):
 // the header walk runs on a helper thread while the stream is copied to the device through the pinned
 // ring (or straight from pinned caller memory); then every complete frame is verified on the device by
 // the arena path over the stream and the verdicts come back.
-int annety_lhc_verify_host(const void* h_stream, size_t size, int length_type, int64_t max_payload,
-                           uint64_t* h_payload_off, uint32_t* h_payload_len, uint8_t* h_ok, size_t max_frames,
-                           size_t* n_frames, size_t* consumed) {
-  if (!n_frames || !consumed || !lhc_type_ok(length_type) || (!h_stream && size) ||
+static int verify_host(const FrameRules& r, const void* h_stream, size_t size, uint64_t* h_payload_off,
+                       uint32_t* h_payload_len, uint8_t* h_ok, size_t max_frames, size_t* n_frames, size_t* consumed) {
+  if (!n_frames || !consumed || !lhc_type_ok(r.T) || (!h_stream && size) ||
       (max_frames && (!h_payload_off || !h_payload_len || !h_ok)))
     return ANNETY_CRC_EINVAL;
   *n_frames = *consumed = 0;
   if (size == 0 || max_frames == 0)
-    return annety_lhc_parse(h_stream, size, length_type, max_payload, h_payload_off, h_payload_len, max_frames,
-                            n_frames, consumed);
+    return parse_frames(r, h_stream, size, h_payload_off, h_payload_len, max_frames, n_frames, consumed);
   DeviceCtx* c = nullptr;
   int rc = current_ctx(&c);
   if (rc) return rc;
@@ -1014,8 +1059,7 @@ int annety_lhc_verify_host(const void* h_stream, size_t size, int length_type, i
   // walk the headers while the bytes go up
   int prc = 0;
   std::thread walker([&] {
-    prc = annety_lhc_parse(h_stream, size, length_type, max_payload, h_payload_off, h_payload_len, max_frames, n_frames,
-                           consumed);
+    prc = parse_frames(r, h_stream, size, h_payload_off, h_payload_len, max_frames, n_frames, consumed);
   });
   auto fail = [&](int status) {
     walker.join();
@@ -1078,6 +1122,18 @@ int annety_lhc_verify_host(const void* h_stream, size_t size, int length_type, i
   const hipError_t e = hipStreamSynchronize(s);
   if (rc == ANNETY_CRC_OK && e != hipSuccess) rc = hip_fail(e);
   return rc ? rc : prc;
+}
+
+int annety_lhc_verify_host(const void* h_stream, size_t size, int length_type, int64_t max_payload,
+                           uint64_t* h_payload_off, uint32_t* h_payload_len, uint8_t* h_ok, size_t max_frames,
+                           size_t* n_frames, size_t* consumed) {
+  return verify_host(lhc_rules(length_type, max_payload), h_stream, size, h_payload_off, h_payload_len, h_ok,
+                     max_frames, n_frames, consumed);
+}
+
+int annety_pbc_verify_host(const void* h_stream, size_t size, uint64_t* h_payload_off, uint32_t* h_payload_len,
+                           uint8_t* h_ok, size_t max_frames, size_t* n_frames, size_t* consumed) {
+  return verify_host(kPbcRules, h_stream, size, h_payload_off, h_payload_len, h_ok, max_frames, n_frames, consumed);
 }
 
 }  // extern "C"

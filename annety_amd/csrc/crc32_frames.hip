@@ -25,22 +25,23 @@ __global__ __launch_bounds__(256) void lhc_compare_kernel(const uint8_t* __restr
     ok[i] = load_be32(stream + off[i] + len[i]) == digest[i] ? 1 : 0;
 }
 
-// One wave per frame: header, payload copy, trailer (LengthHeaderCodec::encode :179-197). Payloads the
-// reference would not write (empty: rt 0 at :169; len > max_payload: rt -1 at :172) are skipped, and
+// One wave per frame: header, payload copy, trailer (LengthHeaderCodec::encode :179-197, ProtobufCodec::
+// encode :235-247). Payloads the reference would not write (empty: rt 0; length outside [enc_min,
+// enc_max]: rt -1) are skipped, and
 // the host plan (annety_lhc_encode_plan) gives them zero bytes in the output.
 // The copy stores aligned dwords; each one is assembled from the two source dwords it straddles with
 // v_alignbyte, so unaligned payloads still move 4 bytes per lane per instruction.
 __global__ __launch_bounds__(256) void lhc_encode_kernel(const uint8_t* __restrict__ src,
                                                          const uint64_t* __restrict__ src_off,
                                                          const uint32_t* __restrict__ len, size_t n, int T,
-                                                         int64_t max_payload, uint8_t* __restrict__ dst,
+                                                         int64_t enc_min, int64_t enc_max, uint8_t* __restrict__ dst,
                                                          const uint64_t* __restrict__ dst_off,
                                                          const uint32_t* __restrict__ digest) {
   const size_t waves = (size_t)gridDim.x * 4;
   const uint32_t lane = threadIdx.x & 63;
   for (size_t i = blockIdx.x * (size_t)4 + (threadIdx.x >> 6); i < n; i += waves) {
     const uint32_t L = len[i];
-    if (L == 0 || (max_payload > 0 && (int64_t)L > max_payload)) continue;
+    if (L == 0 || (int64_t)L < enc_min || (enc_max > 0 && (int64_t)L > enc_max)) continue;
     const uint8_t* s = src + src_off[i];
     uint8_t* d = dst + dst_off[i];
     const uint64_t hdr = (uint64_t)L + 4;  // append_intT(length + 4): low T bytes, big-endian
@@ -78,12 +79,12 @@ hipError_t launch_lhc_compare(const void* stream_base, const uint64_t* off, cons
 }
 
 hipError_t launch_lhc_encode(const void* src, const uint64_t* src_off, const uint32_t* len, size_t n, int T,
-                             int64_t max_payload, void* dst, const uint64_t* dst_off, const uint32_t* digest,
-                             hipStream_t stream) {
+                             int64_t enc_min, int64_t enc_max, void* dst, const uint64_t* dst_off,
+                             const uint32_t* digest, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   const unsigned blocks = (unsigned)((n + 3) / 4 < 8192 ? (n + 3) / 4 : 8192);
   hipLaunchKernelGGL(lhc_encode_kernel, dim3(blocks), dim3(256), 0, stream, static_cast<const uint8_t*>(src),
-                     src_off, len, n, T, max_payload, static_cast<uint8_t*>(dst), dst_off, digest);
+                     src_off, len, n, T, enc_min, enc_max, static_cast<uint8_t*>(dst), dst_off, digest);
   return hipGetLastError();
 }
 

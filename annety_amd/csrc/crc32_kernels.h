@@ -94,8 +94,8 @@ hipError_t launch_arena_lines(const ArenaLaunch& a, hipStream_t stream);
 hipError_t launch_lhc_compare(const void* stream_base, const uint64_t* off, const uint32_t* len, size_t n,
                               const uint32_t* digest, uint8_t* ok, hipStream_t stream);
 hipError_t launch_lhc_encode(const void* src, const uint64_t* src_off, const uint32_t* len, size_t n, int T,
-                             int64_t max_payload, void* dst, const uint64_t* dst_off, const uint32_t* digest,
-                             hipStream_t stream);
+                             int64_t enc_min, int64_t enc_max, void* dst, const uint64_t* dst_off,
+                             const uint32_t* digest, hipStream_t stream);
 int fixed_kernel_block();
 
 }  // namespace annety_crc

@@ -175,6 +175,21 @@ int annety_lhc_encode_batch(const void* d_src, const uint64_t* d_src_off, const 
                             int length_type, int64_t max_payload, void* d_dst, const uint64_t* d_frame_off,
                             void* stream);
 
+/* ---- ProtobufCodec framing, batched (include/protobuf/ProtobufCodec.h, checksum on) ----
+ * The same frame layout with T = 4 and the codec's fixed limits: decode accepts a length field
+ * (payload + 4) in [10, 64 MiB] (min_payload() = nameLen 4 + 2 + checksum 4, :279-283; max_payload()
+ * 64 MiB, unconditional, :273-277; decode :127-173), encode accepts payloads of 6 .. 64 MiB bytes
+ * (:225-247). The CRC covers the whole payload (nameLen + typeName + protobuf bytes, :235-247), so the
+ * message itself stays opaque here: parsing it needs libprotobuf and is the caller's.
+ * Verify with annety_lhc_verify_batch / annety_lhc_verify_stream (format-independent once located). */
+int annety_pbc_parse(const void* h_stream, size_t size, uint64_t* payload_off, uint32_t* payload_len,
+                     size_t max_frames, size_t* n_frames, size_t* consumed);
+int annety_pbc_verify_host(const void* h_stream, size_t size, uint64_t* h_payload_off, uint32_t* h_payload_len,
+                           uint8_t* h_ok, size_t max_frames, size_t* n_frames, size_t* consumed);
+int annety_pbc_encode_plan(const uint32_t* h_len, size_t n, uint64_t* h_frame_off, int8_t* h_rt, uint64_t* total);
+int annety_pbc_encode_batch(const void* d_src, const uint64_t* d_src_off, const uint32_t* d_len, size_t n,
+                            void* d_dst, const uint64_t* d_frame_off, void* stream);
+
 #ifdef __cplusplus
 } /* extern "C" */
 #endif

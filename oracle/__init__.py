@@ -71,6 +71,10 @@ def _load_oracle() -> ctypes.CDLL:
                                       ctypes.c_void_p, _sp]
     lib.oracle_lhc_decode.restype = ctypes.c_int
     lib.oracle_lhc_decode.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_size_t, _sp, _sp, _sp]
+    lib.oracle_pbc_encode.restype = ctypes.c_int
+    lib.oracle_pbc_encode.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p, _sp]
+    lib.oracle_pbc_decode.restype = ctypes.c_int
+    lib.oracle_pbc_decode.argtypes = [ctypes.c_void_p, ctypes.c_size_t, _sp, _sp, _sp]
     return lib
 
 
@@ -212,6 +216,30 @@ def lhc_recv(stream, length_type: int = 4, max_payload: int = DEFAULT_MAX_PAYLOA
             return frames, pos, rt
         frames.append((pos + off, ln))
         pos += used
+
+
+# ---- ProtobufCodec framing (include/protobuf/ProtobufCodec.h) - parity unpinned (needs libprotobuf) ----
+def pbc_encode(payload) -> tuple[int, bytes]:
+    a = _as_u8(payload)
+    out = np.zeros(a.size + 8, dtype=np.uint8)
+    n = ctypes.c_size_t()
+    rt = _lib.oracle_pbc_encode(_ptr(a) if a.size else None, a.size, _ptr(out), ctypes.byref(n))
+    return int(rt), out[: n.value].tobytes()
+
+
+def pbc_recv(stream):
+    """Codec::recv's loop over ProtobufCodec::decode: (frames [(off, len)], consumed, last rt)."""
+    a = _as_u8(stream)
+    frames, pos = [], 0
+    while True:
+        off, ln, used = ctypes.c_size_t(), ctypes.c_size_t(), ctypes.c_size_t()
+        sub = a[pos:]
+        rt = _lib.oracle_pbc_decode(_ptr(sub) if sub.size else None, sub.size, ctypes.byref(off), ctypes.byref(ln),
+                                    ctypes.byref(used))
+        if rt != 1:
+            return frames, pos, int(rt)
+        frames.append((pos + off.value, ln.value))
+        pos += used.value
 
 
 # ---- the compiled reference (only where /root/reference existed at build time) ----

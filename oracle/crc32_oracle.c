@@ -256,3 +256,40 @@ int oracle_crc32_batch_var_mt(const unsigned char* base, const uint64_t* off, co
   for (int t = 0; t < threads; t++) pthread_join(tid[t], NULL);
   return 0;
 }
+
+/* ---- ProtobufCodec framing (include/protobuf/ProtobufCodec.h), checksum enabled ----
+ * Same frame layout as LengthHeaderCodec with length_type() = kLengthType32 (:260-263),
+ * min_payload() = header_length() 4 + 2 + checksum_length() 4 = 10 (:279-283) and
+ * max_payload() = 64 MiB, always enforced (:273-277). Parity is unpinned against the reference
+ * itself (its header needs libprotobuf, absent here); these restate :127-173 and :206-247. */
+#define PBC_MIN_PAYLOAD 10
+#define PBC_MAX_PAYLOAD (64ll * 1024 * 1024)
+
+/* ProtobufCodec::encode (:206-247): 0 for an empty payload, -1 for len < 10 - 4 or len > 64 MiB. */
+int oracle_pbc_encode(const unsigned char* payload, size_t len, unsigned char* out, size_t* out_len) {
+  *out_len = 0;
+  if (len == 0) return 0;                                                              /* :223-225 */
+  if ((int64_t)len < PBC_MIN_PAYLOAD - 4 || (int64_t)len > PBC_MAX_PAYLOAD) return -1; /* :226-230 */
+  put_be(out, 4, (uint64_t)len + 4);                                                  /* :233 */
+  memcpy(out + 4, payload, len);                                                       /* :234 */
+  put_be(out + 4 + len, 4, oracle_crc32_long(payload, len));                          /* :238-247 */
+  *out_len = 4 + len + 4;
+  return 1;
+}
+
+/* ProtobufCodec::decode (:127-173) on `size` readable bytes; as oracle_lhc_decode. */
+int oracle_pbc_decode(const unsigned char* s, size_t size, size_t* payload_off, size_t* payload_len,
+                      size_t* consumed) {
+  *payload_off = *payload_len = *consumed = 0;
+  if (size < 4) return 0;                                                      /* :150 */
+  const int64_t length = (int32_t)(((uint32_t)s[0] << 24) | ((uint32_t)s[1] << 16) | ((uint32_t)s[2] << 8) | s[3]);
+  if (length < PBC_MIN_PAYLOAD || length > PBC_MAX_PAYLOAD) return -1;         /* :152-156 */
+  if (size - 4 < (uint64_t)length) return 0;                                   /* :157 */
+  const unsigned char* tr = s + 4 + length - 4;
+  uint32_t want = ((uint32_t)tr[0] << 24) | ((uint32_t)tr[1] << 16) | ((uint32_t)tr[2] << 8) | tr[3];
+  if (oracle_crc32_long(s + 4, (size_t)length - 4) != want) return -1;         /* :159-173 */
+  *payload_off = 4;
+  *payload_len = (size_t)length - 4;
+  *consumed = 4 + (size_t)length;
+  return 1;
+}

@@ -25,7 +25,7 @@ def H(x: str) -> int:
 def declared_symbols():
     src = open(HEADER).read()
     src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(annety_(?:crc|lhc)\w*)\s*\(", src)))
+    return sorted(set(re.findall(r"\b(annety_(?:crc|lhc|pbc)\w*)\s*\(", src)))
 
 
 def test_library_exports_every_declared_symbol():
