@@ -1,18 +1,30 @@
 // Arena path for variable-length batches whose payloads lie in one buffer (a NetBuffer, a frame
 // stream, a packed batch: BASELINE config 3). Two launches, no sort:
 //
-//  1. crc32_arena_lines_kernel streams EVERY 128-byte line of the arena, payload-agnostic, in the
-//     access shape of the config-1 kernel (a wave reads 64 consecutive lines = one 8 KiB superblock
-//     per round). Per line it writes the raw CRC (register 0, no init, no xorout) c1, per aligned
-//     1 KiB block c8 = join of 8 lines, per 8 KiB superblock c64 = join of 8 blocks. No byte masks,
-//     no per-payload state: the arena runs at the fixed-batch rate whatever the length mix.
-//  2. crc32_arena_stitch_kernel gives one lane per payload. The payload's first and last lines are
-//     folded from the data with byte masks; the lines between come from c1/c8/c64 by Horner's rule
-//         acc = shift_|unit|(acc) ^ crc(unit),   units of 128 B, 1 KiB and 8 KiB,
-//     so a 64 KiB payload takes at most ~34 steps of 8 nibble-table lookups. The register before
-//     the payload enters as shift_{128-lead}(s) (s = 0xFFFFFFFF, or the caller's register in update
-//     mode, include/Crc32c.h:71-82), and the zero bytes after the payload end in its last line are
-//     removed by one inverse shift.
+//  1. The line pass (crc32_oneround_kernel<8> in ARENA mode, crc32_kernels.hip) streams EVERY 128-byte
+//     line of the arena, payload-agnostic, in the access shape of the config-1 kernel (a wave reads 64
+//     consecutive lines = one 8 KiB superblock per round). Per line j of a 1 KiB block it stores the
+//     block-suffix CRC S[j] = raw(lines j..7) (register 0, no init), per block g of a superblock the
+//     superblock-suffix SB[g] = raw(blocks g..7). No payload state: the arena runs at the fixed-batch
+//     rate whatever the length mix.
+//  2. crc32_arena_stitch_kernel gives one lane per payload. With V(x) the register after the bytes
+//     before address x, taken as data (a "virtual" register that equals the payload's register inside
+//     it), the payload [A, E) reads as
+//         V at a line boundary  ->  whole lines I0..I1 from S/SB  ->  V(E)
+//     and only two half-line (64-byte) windows are folded from the data:
+//       head: lead = A % 128 < 64: the bytes [line start, A) of the first line, which fix V(first line
+//             start) = shift_{-lead}(s ^ raw(them)); else the payload's bytes [A, line end), which give
+//             V(first line end) = shift_{128-lead}(s) ^ raw(them);
+//       tail: te = bytes of the last line up to E >= 64: the bytes [E, line end), removed from V(last
+//             line end) as V(E) = shift_{-(128-te)}(V ^ raw(them)); else the payload's bytes [line start,
+//             E), appended to V(last line start).
+//     The whole lines between take at most four steps acc = M1(acc) ^ M2(S[a] ^ S[b]) (the head block,
+//     the partial superblocks' block runs, the tail block: M1 = shift by the unit, M2 = the inverse
+//     shift that cuts a suffix difference down to the unit) and one step per whole superblock between.
+//     A config-3 payload (6.5 KiB on average) costs 64 + 64 bytes of window folds and about six map
+//     steps of 8 nibble-table lookups, with every load issued before the first fold.
+//     s = 0xFFFFFFFF (crc32_long) or the caller's register (crc32_update, include/Crc32c.h:71-82).
+//     Bytes outside the arena [byte_lo, byte_hi) sharing a line with it are zeros to both launches.
 //
 // Reference semantics: crc32_long include/Crc32c.h:58-69 (digests), crc32_update :71-82 (update
 // mode); the math identities are in crc32_math.h. DESIGN.md §2.8.
@@ -27,183 +39,283 @@
 namespace annety_crc {
 namespace {
 
-// 512 lanes per block (one block per CU, LDS-bound), which leaves 256 VGPRs for the four-chain edge
-// fold; a config-3 batch (165k payloads) is 1.26 payloads per lane. (1024-lane blocks, which cap the kernel at 128 VGPRs, returned wrong digests
-// for whole waves now and then on the MI355X - a register-pressure-dependent fault we did not pin
-// down)
+// 512 lanes per block (one block per CU, LDS-bound), which leaves 256 VGPRs per lane; a config-3 batch
+// (165k payloads) is 1.26 payloads per lane. (1024-lane blocks, which cap a kernel at 128 VGPRs,
+// returned wrong digests for whole waves now and then on the MI355X with the previous stitch - a
+// register-pressure-dependent fault we did not pin down)
 constexpr int kStitchBlock = 512;
 
-// Keep bytes [lo8/8, hi8/8) of a 128-byte line, zero the rest (branch-free, per 32-bit word).
-__device__ __forceinline__ void mask_line(uint4 (&v)[8], int32_t lo8, int32_t hi8) {
+// Map i of a set of T nibble-table maps stored [k][i][v] (k nibble position, v value): for one k the
+// set's tables lie side by side, so lanes applying different maps spread over the banks
+// ((16 i + v) mod 64) instead of all sharing the same 16 (a [i][k][v] layout cost the segment steps
+// up to 8-way conflicts).
+template <uint32_t T>
+__device__ __forceinline__ uint32_t nibble_map_set(uint32_t s, const uint32_t* lds, uint32_t off, uint32_t i) {
+  const uint32_t* t = lds + off / 4 + i * 16;
+  uint32_t r[8];
 #pragma unroll
-  for (int i = 0; i < 8; i++) {
-    uint32_t* w = reinterpret_cast<uint32_t*>(&v[i]);
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const int32_t p8 = (i * 16 + q * 4) * 8;
-      const uint32_t keep_lo = (uint32_t)(0xFFFFFFFFull << clamp032(lo8 - p8));
-      const uint32_t keep_hi = (uint32_t)(0xFFFFFFFFull >> clamp032(p8 + 32 - hi8));
-      w[q] &= keep_lo & keep_hi;
-    }
-  }
+  for (int k = 0; k < 8; k++) r[k] = t[k * T * 16 + __builtin_amdgcn_ubfe(s, 4 * k, 4)];
+  return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6] ^ r[7]);
 }
-
 // shift_{-m} for m in [0, 128): U_hi[m >> 4] o U_lo[m & 15]
 __device__ __forceinline__ uint32_t unshift(uint32_t t, uint32_t m, const uint32_t* lds) {
-  t = nibble_map_uniform(t, lds, kLdsStitchUnshiftOff + (m & 15u) * 512);
-  return nibble_map_uniform(t, lds, kLdsStitchUnshiftOff + 8192 + (m >> 4) * 512);
+  t = nibble_map_set<16>(t, lds, kLdsStitchUnshiftOff, m & 15u);
+  return nibble_map_set<8>(t, lds, kLdsStitchUnshiftOff + 8192, m >> 4);
+}
+__device__ __forceinline__ uint32_t seg_map(uint32_t t, uint32_t idx, const uint32_t* lds) {
+  return nibble_map_set<32>(t, lds, kLdsMapOff, idx);
 }
 
 __device__ __forceinline__ uint32_t gload4(uint64_t addr) {
   return *(const __attribute__((address_space(1))) uint32_t*)addr;
 }
 
-//   PROBE (microbench only; product = 0): 1 = descriptors and stores only, 2 = + edge-line loads,
-//   3 = + edge folds (no interior steps), 4 = full but single-chain folds (absorb_line twice) - wrong
-//   digests for 1-3, used to measure what the stages cost.
+// Two 64-byte windows from register 0, four 32-byte chains: raw(window) = shift_32(raw(first half)) ^
+// raw(second half).
+__device__ __forceinline__ void absorb_two_windows(const uint4 (&v)[4], const uint4 (&w)[4], const LaneCtx& k,
+                                                   const uint32_t* lds, uint32_t& rv, uint32_t& rw) {
+  uint32_t xa = v[0].x, xb = v[2].x, xc = w[0].x, xd = w[2].x;
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    word4x4(xa, v[i].y, xb, v[2 + i].y, xc, w[i].y, xd, w[2 + i].y, k);
+    word4x4(xa, v[i].z, xb, v[2 + i].z, xc, w[i].z, xd, w[2 + i].z, k);
+    word4x4(xa, v[i].w, xb, v[2 + i].w, xc, w[i].w, xd, w[2 + i].w, k);
+    word4x4(xa, i == 0 ? v[1].x : 0u, xb, i == 0 ? v[3].x : 0u, xc, i == 0 ? w[1].x : 0u, xd, i == 0 ? w[3].x : 0u, k);
+  }
+  rv = nibble_map_uniform(xa, lds, kLdsQuarterOff) ^ xb;
+  rw = nibble_map_uniform(xc, lds, kLdsQuarterOff) ^ xd;
+}
+
+struct StitchArgs {
+  const uint8_t* base;
+  uint64_t byte_lo, byte_hi, line_lo, line_hi, sb0, fs0, fs1;
+  uint32_t lg;
+  const uint32_t *S, *SB, *S_edge;
+  const uint64_t* off;
+  const uint32_t* len;
+  size_t n;
+  const uint4* img_slice;
+  const uint4* img_stitch;
+  uint64_t zero_line;
+  uint32_t* out;
+};
+
+// One payload's loads and the plan that consumes them. Steps 0..3 = head block, first partial
+// superblock's blocks, last partial superblock's blocks, tail block; mid = whole superblocks between.
+struct Plan {
+  uint64_t A, E;
+  uint32_t len;
+  bool fast, headX, tailX;
+  uint32_t lead, te;
+  uint32_t hlo, hhi, tlo, thi;  // window byte ranges kept, relative to the window start
+  uint32_t m1[4], m2[4];        // step maps (seg_map index)
+  uint32_t act, yzero;          // per step bit: active / second operand is zero
+  uint32_t nmid;
+  uint64_t mid_s;               // first whole superblock between (relative to sb0)
+};
+struct Vals {
+  uint4 h[4], t[4];
+  uint32_t x[4], y[4], mid[8];
+  uint32_t s0;
+};
+
+//   PROBE (microbench only; product = 0): 1 = descriptors and stores only, 2 = + all loads,
+//   3 = + window folds (no map steps) - wrong digests, used to measure what the stages cost.
 template <bool UPD, int BLK = kStitchBlock, int PROBE = 0>
-__global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(
-    const uint8_t* __restrict__ base, uint64_t line_lo, uint64_t line_hi, uint64_t sb0,
-    const uint64_t* __restrict__ d_off, const uint32_t* __restrict__ d_len, size_t n,
-    const uint32_t* __restrict__ c1, const uint32_t* __restrict__ c8, const uint32_t* __restrict__ c64,
-    const uint4* __restrict__ img_slice, const uint4* __restrict__ img_stitch, uint32_t* __restrict__ out) {
+__global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchArgs g) {
   __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsStitchImageBytes / 16];
   const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
   LaneCtx k;
   k.L0 = (threadIdx.x & 31) << 3;
   k.L1 = k.L0 | (1u << 16);
   k.slot4 = (threadIdx.x & 31) << 2;
-  const uint64_t c1b = (uint64_t)(uintptr_t)c1 - 4 * (sb0 * 64);
-  const uint64_t c8b = (uint64_t)(uintptr_t)c8 - 4 * (sb0 * 8);
-  const uint64_t c64b = (uint64_t)(uintptr_t)c64 - 4 * sb0;
+  const uint64_t gmask = ((uint64_t)1 << g.lg) - 1;
+  const uint64_t s_base = (uint64_t)(uintptr_t)g.S, e_base = (uint64_t)(uintptr_t)g.S_edge;
+  const uint64_t sb_base = (uint64_t)(uintptr_t)g.SB;
 
-  struct Pay {
-    uint64_t L0, L1;
-    uint32_t lead, tailend, len;
+  // address of S for line a (0..7) of block rb (relative to superblock sb0): task-major bursts for the
+  // full superblocks (crc32_kernels.h kSTasks), S_edge for the partial ones
+  auto s_addr = [&](uint64_t rb, uint32_t a) -> uint64_t {
+    const uint64_t sb = g.sb0 + (rb >> 3);
+    const bool edge = sb < g.fs0 || sb >= g.fs1;
+    const uint64_t r = rb - (g.fs0 - g.sb0) * 8;
+    const uint64_t t = r >> g.lg;
+    const uint64_t burst = arena_s_word(t, r & gmask, a, g.lg) * 4;
+    const uint64_t ed = ((sb == g.sb0 ? 0 : 64) + (rb & 7) * 8 + a) * 4;
+    return edge ? e_base + ed : s_base + burst;
   };
-  auto describe = [&](size_t p) {
-    Pay y;
-    y.len = d_len[p];
-    const uint64_t a = (uint64_t)(uintptr_t)base + d_off[p];
-    const uint64_t e = a + (y.len ? y.len - 1 : 0);
-    y.L0 = a >> 7;
-    y.L1 = e >> 7;
-    y.lead = (uint32_t)(a & 127);
-    y.tailend = (uint32_t)(e & 127) + 1;
-    return y;
-  };
-  // Horner steps over interior lines [i, L1) from the arena pass: 8 independent loads per batch, then 8
-  // steps acc = shift_unit(acc) ^ crc(unit) with units of 8 KiB / 1 KiB / 128 B (lv = 2 / 1 / 0, 3 = none)
-  auto fetch = [&](uint64_t& i, uint64_t L1, uint32_t (&cv)[8], uint32_t& lv) {  // lv: 2 bits per step
-    lv = 0;
+  auto sb_addr = [&](uint64_t sbr, uint32_t gg) -> uint64_t { return sb_base + (sbr * 8 + gg) * 4; };
+
+  auto plan_and_load = [&](size_t p, Plan& y, Vals& v) {
+    y.len = g.len[p];
+    y.A = (uint64_t)(uintptr_t)g.base + g.off[p];
+    y.E = y.A + y.len;
+    const uint64_t dummy = (uint64_t)(uintptr_t)(g.len + p);
+    y.fast = y.len > 0 && y.A >= g.byte_lo && y.E <= g.byte_hi;
+    const uint64_t L0 = y.A >> 7, L1 = (y.E - (y.len ? 1 : 0)) >> 7;
+    y.lead = (uint32_t)(y.A & 127);
+    y.te = (uint32_t)((y.E - (y.len ? 1 : 0)) & 127) + (y.len ? 1u : 0u);
+    y.headX = y.lead < 64;
+    y.tailX = y.te >= 64;
+    const uint32_t cl0 = L0 == g.line_lo ? (uint32_t)(g.byte_lo & 127) : 0u;
+    const uint32_t ch0 = L0 == g.line_hi ? (uint32_t)(((g.byte_hi - 1) & 127) + 1) : 128u;
+    const uint32_t cl1 = L1 == g.line_lo ? (uint32_t)(g.byte_lo & 127) : 0u;
+    const uint32_t ch1 = L1 == g.line_hi ? (uint32_t)(((g.byte_hi - 1) & 127) + 1) : 128u;
+    // windows: head [0,64) keeps [cl, lead) or [64,128) keeps [lead, ch); tail [64,128) keeps [te, ch) or
+    // [0,64) keeps [cl, te)
+    const uint32_t oh = y.headX ? 0u : 64u, ot = y.tailX ? 64u : 0u;
+    y.hlo = (y.headX ? cl0 : y.lead) - oh;
+    y.hhi = (y.headX ? y.lead : ch0) - oh;
+    y.tlo = (y.tailX ? y.te : cl1) - ot;
+    y.thi = (y.tailX ? ch1 : y.te) - ot;
+    const uint64_t hsrc = y.len ? (L0 << 7) + oh : g.zero_line;
+    const uint64_t tsrc = y.len ? (L1 << 7) + ot : g.zero_line;
 #pragma unroll
-    for (int q = 0; q < 8; q++) {
-      const bool big = (i & 63) == 0 && i + 64 <= L1;
-      const bool mid = !big && (i & 7) == 0 && i + 8 <= L1;
-      const bool any = i < L1;
-      lv |= (any ? (big ? 2u : (mid ? 1u : 0u)) : 3u) << (2 * q);
-      const uint64_t addr = big ? c64b + 4 * (i >> 6) : (mid ? c8b + 4 * (i >> 3) : c1b + 4 * (any ? i : L1 - 1));
-      cv[q] = gload4(addr);
-      i += any ? (big ? 64 : (mid ? 8 : 1)) : 0;
-    }
-  };
-  auto apply = [&](uint32_t acc, const uint32_t (&cv)[8], uint32_t lv) {
+    for (int i = 0; i < 4; i++) v.h[i] = gload16(hsrc + 16 * i);
 #pragma unroll
-    for (int q = 0; q < 8; q++) {
-      const uint32_t l = (lv >> (2 * q)) & 3u;
-      if (l < 3) acc = nibble_map_uniform(acc, lds, kLdsLevelOff + l * 512) ^ cv[q];
+    for (int i = 0; i < 4; i++) v.t[i] = gload16(tsrc + 16 * i);
+
+    // whole lines I0..I1 (empty when I1 < I0)
+    const int64_t I0 = (int64_t)L0 + (y.headX ? 0 : 1), I1 = (int64_t)L1 - (y.tailX ? 0 : 1);
+    const bool seg = y.fast && I1 >= I0;
+    const uint64_t b0 = (uint64_t)I0 >> 3, b1 = (uint64_t)I1 >> 3;
+    const uint32_t a = (uint32_t)I0 & 7, z = (uint32_t)I1 & 7;
+    const uint64_t rb0 = b0 - g.sb0 * 8, rb1 = b1 - g.sb0 * 8;
+    const bool same = b0 == b1;
+    const bool blocks = seg && b1 >= b0 + 2;
+    const uint64_t B0 = rb0 + 1, B1 = rb1 - 1;
+    const uint64_t s0 = B0 >> 3, s1 = B1 >> 3;
+    const uint32_t g0 = (uint32_t)B0 & 7, g1 = (uint32_t)B1 & 7;
+    const bool one = s0 == s1;
+    uint64_t xa[4], ya[4];
+    // step 0: head block (or the whole run when it stays in one block)
+    y.m1[0] = kMapF + (same ? z - a + 1 : 8 - a) - 1;
+    y.m2[0] = kMapUL + (same ? 7 - z : 0);
+    xa[0] = s_addr(rb0, a);
+    ya[0] = s_addr(rb0, z + 1 < 8 ? z + 1 : 0);
+    bool yz0 = !same || z == 7;
+    // step 1: blocks of the first partial superblock (or all of them when they stay in one)
+    y.m1[1] = kMapG + (one ? g1 - g0 + 1 : 8 - g0) - 1;
+    y.m2[1] = kMapUB + (one ? 7 - g1 : 0);
+    xa[1] = sb_addr(s0, g0);
+    ya[1] = sb_addr(s0, g1 + 1 < 8 ? g1 + 1 : 0);
+    bool yz1 = !one || g1 == 7;
+    // step 2: blocks 0..g1 of the last partial superblock
+    y.m1[2] = kMapG + g1;
+    y.m2[2] = kMapUB + (7 - g1);
+    xa[2] = sb_addr(s1, 0);
+    ya[2] = sb_addr(s1, g1 + 1 < 8 ? g1 + 1 : 0);
+    bool yz2 = g1 == 7;
+    // step 3: lines 0..z of the tail block
+    y.m1[3] = kMapF + z;
+    y.m2[3] = kMapUL + (7 - z);
+    xa[3] = s_addr(rb1, 0);
+    ya[3] = s_addr(rb1, z + 1 < 8 ? z + 1 : 0);
+    bool yz3 = z == 7;
+    y.act = (seg ? 1u : 0u) | (blocks ? 2u : 0u) | (blocks && !one ? 4u : 0u) | (seg && !same ? 8u : 0u);
+    y.yzero = (yz0 ? 1u : 0u) | (yz1 ? 2u : 0u) | (yz2 ? 4u : 0u) | (yz3 ? 8u : 0u);
+    y.nmid = blocks && !one ? (uint32_t)(s1 - s0 - 1) : 0u;
+    y.mid_s = s0 + 1;
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const bool on = (y.act >> q) & 1u;
+      v.x[q] = gload4(on ? xa[q] : dummy);
+      v.y[q] = gload4(on && !((y.yzero >> q) & 1u) ? ya[q] : dummy);
     }
-    return acc;
+#pragma unroll
+    for (int q = 0; q < 8; q++) v.mid[q] = gload4((uint32_t)q < y.nmid ? sb_addr(y.mid_s + q, 0) : dummy);
+    v.s0 = UPD ? gload4((uint64_t)(uintptr_t)(g.out + p)) : kInit;
   };
-  auto process = [&](size_t p, const Pay& y, uint4 (&v)[8], uint4 (&w)[8]) {
+
+  auto process = [&](size_t p, const Plan& y, Vals& v) {
     if (y.len == 0) {  // crc of the empty string is 0; update mode leaves the register alone
-      if constexpr (!UPD) out[p] = 0u;
+      if constexpr (!UPD) g.out[p] = 0u;
       return;
     }
-    const uint32_t s0 = UPD ? out[p] : kInit;
     if constexpr (PROBE == 1) {
-      out[p] = (uint32_t)y.L0 ^ y.lead ^ s0;
+      g.out[p] = (uint32_t)y.A ^ y.lead ^ v.s0;
       return;
     }
     if constexpr (PROBE == 2) {
-      uint32_t t = 0;
+      uint32_t t = v.s0;
 #pragma unroll
-      for (int q = 0; q < 8; q++) t ^= v[q].x ^ w[q].y;
-      out[p] = t;
+      for (int q = 0; q < 4; q++) t ^= v.h[q].x ^ v.t[q].y ^ v.x[q] ^ v.y[q];
+#pragma unroll
+      for (int q = 0; q < 8; q++) t ^= v.mid[q];
+      g.out[p] = t;
       return;
     }
-    const bool interior = y.L1 >= y.L0 + 2;
-    const bool arena = y.L0 + 1 >= line_lo && y.L1 - 1 <= line_hi;
-    uint64_t i = y.L0 + 1;
-    uint32_t cv[8], cv2[8], lv = 0, lv2 = 0;
-    if (PROBE != 3 && interior && arena) {  // first 16 steps in flight during the edge folds
-      fetch(i, y.L1, cv, lv);
-      fetch(i, y.L1, cv2, lv2);
-    }
-    // edge lines: the first keeps [lead, 128) (or [lead, tailend) when it is also the last), the last
-    // keeps [0, tailend); both folded together (a single-line payload folds its line twice, unused)
-    mask_line(v, (int32_t)y.lead * 8, (int32_t)(y.L0 == y.L1 ? y.tailend : 128u) * 8);
-    mask_line(w, 0, (int32_t)y.tailend * 8);
-    uint32_t acc, x;
-    if constexpr (PROBE == 4) {
-      acc = absorb_line(0u, v, k, lds);
-      x = absorb_line(0u, w, k, lds);
-    } else {
-      absorb_two_lines(v, w, k, lds, acc, x);
-    }
-    // register before the payload: raw(P, s) = shift_|P|(s) ^ raw(P, 0), |P| = 128 - lead
-    acc ^= unshift(nibble_map_uniform(s0, lds, kLdsLevelOff), y.lead, lds);
-    if (y.L1 > y.L0) {
-      if (PROBE == 3) {
-      } else if (interior && arena) {
-        acc = apply(acc, cv, lv);
-        acc = apply(acc, cv2, lv2);
-        while (i < y.L1) {
-          fetch(i, y.L1, cv, lv);
-          fetch(i, y.L1, cv2, lv2);
-          acc = apply(acc, cv, lv);
-          acc = apply(acc, cv2, lv2);
-        }
-      } else {
-        // payload reaches outside the arena the caller declared: fold its interior lines directly
-        for (; i < y.L1; i++) {
-          uint4 u[8];
+    uint32_t acc;
+    if (y.fast) {
+      mask_line<4>(v.h, (int32_t)y.hlo * 8, (int32_t)y.hhi * 8);
+      mask_line<4>(v.t, (int32_t)y.tlo * 8, (int32_t)y.thi * 8);
+      uint32_t wh, wt;
+      absorb_two_windows(v.h, v.t, k, lds, wh, wt);
+      // head: V(first line start) = shift_{-lead}(s0) ^ shift_{-64}(wh), or
+      //       V(first line end) = shift_{-lead}(shift_128(s0)) ^ wh
+      const uint32_t f1s = seg_map(v.s0, kMapF, lds);
+      const uint32_t u64 = nibble_map_set<8>(wh, lds, kLdsStitchUnshiftOff + 8192, 4);  // shift_{-64}
+      acc = unshift(y.headX ? v.s0 : f1s, y.lead, lds) ^ (y.headX ? u64 : wh);
+      if constexpr (PROBE != 3) {
 #pragma unroll
-          for (int q = 0; q < 8; q++) u[q] = gload16((i << 7) + 16 * q);
-          acc = nibble_map_uniform(acc, lds, kLdsLevelOff) ^ absorb_line(0u, u, k, lds);
+        for (int q = 0; q < 2; q++) {
+          if ((y.act >> q) & 1u) {
+            const uint32_t d = v.x[q] ^ (((y.yzero >> q) & 1u) ? 0u : v.y[q]);
+            acc = seg_map(acc, y.m1[q], lds) ^ seg_map(d, y.m2[q], lds);
+          }
+        }
+        // whole superblocks between the partial ones: acc = shift_8KiB(acc) ^ SB[s,0]
+        for (uint32_t i = 0; i < y.nmid; i += 8) {
+          if (i > 0) {
+#pragma unroll
+            for (int q = 0; q < 8; q++) v.mid[q] = gload4(sb_addr(y.mid_s + (i + q < y.nmid ? i + q : i), 0));
+          }
+#pragma unroll
+          for (int q = 0; q < 8; q++)
+            if (i + q < y.nmid) acc = seg_map(acc, kMapG + 7, lds) ^ v.mid[q];
+        }
+#pragma unroll
+        for (int q = 2; q < 4; q++) {
+          if ((y.act >> q) & 1u) {
+            const uint32_t d = v.x[q] ^ (((y.yzero >> q) & 1u) ? 0u : v.y[q]);
+            acc = seg_map(acc, y.m1[q], lds) ^ seg_map(d, y.m2[q], lds);
+          }
         }
       }
-      acc = nibble_map_uniform(acc, lds, kLdsLevelOff) ^ x;
+      // tail: V(E) = shift_{-(128-te)}(V(last line end) ^ wt), or
+      //       shift_{-(128-te)}(shift_128(V(last line start)) ^ shift_64(wt))
+      const uint32_t f1a = seg_map(acc, kMapF, lds);
+      const uint32_t h64 = nibble_map_uniform(wt, lds, kLdsHalfOff);
+      acc = unshift(y.tailX ? acc ^ wt : f1a ^ h64, 128 - y.te, lds);
+    } else {
+      // payload reaches outside the arena the caller declared (or there is none): fold its lines directly
+      const uint64_t L0 = y.A >> 7, L1 = (y.E - 1) >> 7;
+      acc = unshift(v.s0, y.lead, lds);  // V(first line start): the lead bytes are zeros here
+      for (uint64_t i = L0; i <= L1; i++) {
+        uint4 u[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) u[q] = gload16((i << 7) + 16 * q);
+        mask_line<8>(u, i == L0 ? (int32_t)y.lead * 8 : 0, i == L1 ? (int32_t)y.te * 8 : 1024);
+        acc = seg_map(acc, kMapF, lds) ^ absorb_line(0u, u, k, lds);
+      }
+      acc = unshift(acc, 128 - y.te, lds);  // drop the zero bytes after the payload end
     }
-    acc = unshift(acc, 128 - y.tailend, lds);  // drop the zero bytes after the payload end
-    out[p] = UPD ? acc : ~acc;
-  };
-  auto load_edges = [&](const Pay& y, uint4 (&v)[8], uint4 (&w)[8]) {
-#pragma unroll
-    for (int i = 0; i < 8; i++) v[i] = gload16((y.L0 << 7) + 16 * i);
-#pragma unroll
-    for (int i = 0; i < 8; i++) w[i] = gload16((y.L1 << 7) + 16 * i);
+    g.out[p] = UPD ? acc : ~acc;
   };
 
   // contiguous payload ranges per block (coalesced descriptor loads), the same count for every block;
-  // the first payload's descriptor and edge lines are in flight while the LDS image is staged
-  const size_t per = (n + gridDim.x - 1) / gridDim.x;
-  const size_t p_end = std::min(n, (size_t)(blockIdx.x + 1) * per);
-  size_t p = (size_t)blockIdx.x * per + threadIdx.x;
-  Pay y{};
-  uint4 v[8], w[8];
-  if (p < p_end) {
-    y = describe(p);
-    load_edges(y, v, w);
-  }
-  load_image<kLdsStitchImageBytes, BLK, kLdsCommonBytes>(lds4, img_slice, nullptr, img_stitch);
+  // the first payload's loads are in flight while the LDS image is staged
+  const size_t per = (g.n + gridDim.x - 1) / gridDim.x;
+  const size_t p_end = std::min(g.n, (size_t)(blockIdx.x + 1) * per);
+  const size_t p_first = (size_t)blockIdx.x * per + threadIdx.x;
+  Plan y{};
+  Vals v{};
+  if (p_first < p_end) plan_and_load(p_first, y, v);
+  load_image<kLdsStitchImageBytes, BLK, kLdsCommonBytes>(lds4, g.img_slice, nullptr, g.img_stitch);
   __syncthreads();
-  for (; p < p_end; p += BLK) {
-    if (p != (size_t)blockIdx.x * per + threadIdx.x) {
-      y = describe(p);
-      load_edges(y, v, w);
-    }
-    process(p, y, v, w);
+  for (size_t p = p_first; p < p_end; p += BLK) {
+    if (p != p_first) plan_and_load(p, y, v);
+    process(p, y, v);
   }
 }
 
@@ -213,21 +325,45 @@ size_t stitch_blocks(const ArenaLaunch& a) {
   return std::max<size_t>(1, std::min<size_t>(a.max_blocks, (a.n + kStitchBlock - 1) / kStitchBlock));
 }
 
+template <int PROBE>
+hipError_t launch_stitch_p(const ArenaLaunch& a, hipStream_t stream) {
+  const ArenaGeom geo = arena_geom(a);
+  StitchArgs s;
+  s.base = static_cast<const uint8_t*>(a.base);
+  s.byte_lo = a.byte_lo;
+  s.byte_hi = a.byte_hi;
+  s.line_lo = a.line_lo;
+  s.line_hi = a.line_hi;
+  s.sb0 = a.sb0;
+  s.fs0 = a.fs0;
+  s.fs1 = a.fs1;
+  s.lg = geo.lg;
+  s.S = a.scratch;
+  s.SB = a.scratch ? a.scratch + geo.sb_off : nullptr;
+  s.S_edge = a.scratch ? a.scratch + geo.edge_off : nullptr;
+  s.off = a.off;
+  s.len = a.len;
+  s.n = a.n;
+  s.img_slice = static_cast<const uint4*>(a.img_slice);
+  s.img_stitch = static_cast<const uint4*>(a.img_stitch);
+  s.zero_line = (uint64_t)(uintptr_t)a.zero_line;
+  s.out = a.out;
+  const size_t blocks = stitch_blocks(a);
+  if (a.update)
+    hipLaunchKernelGGL((crc32_arena_stitch_kernel<true, kStitchBlock, PROBE>), dim3((unsigned)blocks),
+                       dim3(kStitchBlock), 0, stream, s);
+  else
+    hipLaunchKernelGGL((crc32_arena_stitch_kernel<false, kStitchBlock, PROBE>), dim3((unsigned)blocks),
+                       dim3(kStitchBlock), 0, stream, s);
+  return hipGetLastError();
+}
+
 hipError_t launch_arena(const ArenaLaunch& a, hipStream_t stream) {
   if (a.nsb) {
     const hipError_t e = launch_arena_lines(a, stream);  // crc32_kernels.hip
     if (e != hipSuccess) return e;
   }
-  const size_t blocks = stitch_blocks(a);
-#define ANNETY_STITCH(UPD)                                                                                     \
-  hipLaunchKernelGGL((crc32_arena_stitch_kernel<UPD>), dim3((unsigned)blocks), dim3(kStitchBlock), 0, stream,  \
-                     static_cast<const uint8_t*>(a.base), a.line_lo, a.line_hi, a.sb0, a.off, a.len, a.n, a.c1,   \
-                     a.c8, a.c64, static_cast<const uint4*>(a.img_slice), static_cast<const uint4*>(a.img_stitch), \
-                     a.out)
-  if (a.update) ANNETY_STITCH(true);
-  else ANNETY_STITCH(false);
-#undef ANNETY_STITCH
-  return hipGetLastError();
+  return launch_stitch_p<0>(a, stream);
 }
 
 }  // namespace annety_crc

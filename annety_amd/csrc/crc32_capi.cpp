@@ -170,7 +170,7 @@ struct HostImages {
   std::vector<uint32_t> groups;  // kNumGroups * (kGroupImageBytes / 4)
   std::vector<uint32_t> unshift; // 24 maps x 128 words (U_lo[0..15], U_hi[0..7])
   std::vector<uint32_t> sb;      // arena superblock join: (k, v, g) = shift_{(7-g)*1024}(v << 4k)
-  std::vector<uint32_t> stitch;  // arena stitch: level maps shift_{128*8^L} (3 x 128 words) + unshift
+  std::vector<uint32_t> stitch;  // arena stitch: segment maps F/G/UL/UB, unshift, shift_32 (crc32_math.h)
   uint32_t short_init[4];
 };
 
@@ -261,8 +261,31 @@ const HostImages& host_images() {
         for (int v = 0; v < 16; v++) img.sb[kk * 128 + v * 8 + g] = nt[kk * 16 + v];
     }
     img.stitch.assign((kLdsStitchImageBytes - kLdsCommonBytes) / 4, 0);
-    for (int L = 0; L < 3; L++) nibble_tables(shift_matrix((uint64_t)128 << (3 * L)), img.stitch.data() + L * 128);
-    std::memcpy(img.stitch.data() + kLdsLevelBytes / 4, img.unshift.data(), img.unshift.size() * 4);
+    {
+      // sets of maps stored [k][i][v] (crc32_arena.hip nibble_map_set)
+      auto put_set = [](uint32_t* dst, const uint32_t* maps /* [i][k][v] */, uint32_t T) {
+        for (uint32_t i = 0; i < T; i++)
+          for (uint32_t kk = 0; kk < 8; kk++)
+            for (uint32_t v = 0; v < 16; v++) dst[(kk * T + i) * 16 + v] = maps[i * 128 + kk * 16 + v];
+      };
+      std::vector<uint32_t> seg(32 * 128);
+      const Gf2Mat inv128 = gf2_inverse(shift_matrix(128)), inv1024 = gf2_inverse(shift_matrix(1024));
+      Gf2Mat ul{}, ub{};
+      for (int i = 0; i < 32; i++) ul.col[i] = ub.col[i] = 1u << i;
+      for (uint32_t q = 0; q < 8; q++) {
+        nibble_tables(shift_matrix((uint64_t)128 * (q + 1)), seg.data() + (kMapF + q) * 128);   // F(q+1)
+        nibble_tables(shift_matrix((uint64_t)1024 * (q + 1)), seg.data() + (kMapG + q) * 128);  // G(q+1)
+        nibble_tables(ul, seg.data() + (kMapUL + q) * 128);                                      // UL(q)
+        nibble_tables(ub, seg.data() + (kMapUB + q) * 128);                                      // UB(q)
+        ul = gf2_mul(inv128, ul);
+        ub = gf2_mul(inv1024, ub);
+      }
+      uint32_t* m = img.stitch.data();
+      put_set(m, seg.data(), 32);
+      put_set(m + (kLdsStitchUnshiftOff - kLdsMapOff) / 4, img.unshift.data(), 16);                  // U_lo
+      put_set(m + (kLdsStitchUnshiftOff + 8192 - kLdsMapOff) / 4, img.unshift.data() + 16 * 128, 8);  // U_hi
+      nibble_tables(shift_matrix(32), m + (kLdsQuarterOff - kLdsMapOff) / 4);
+    }
   });
   return img;
 }
@@ -297,6 +320,17 @@ struct DeviceCtx {
   std::mutex stg_mu;  // one host-staged batch at a time per device
   std::mutex pow_mu;  // split-path power tables, one per segment size
   std::vector<std::pair<uint64_t, uint32_t*>> powers;
+  // arena-path scratch, reused across calls (run_arena): each slot's last use is fenced by an event that
+  // a later call on any stream waits for, so reuse is safe whatever streams the callers use
+  struct ScratchSlot {
+    void* ptr = nullptr;
+    size_t bytes = 0;
+    hipStream_t last = nullptr;
+    hipEvent_t done = nullptr;
+  };
+  std::mutex arena_mu;  // held while a call picks a slot and enqueues its two launches
+  ScratchSlot arena_slot[8];
+  int arena_slots = 0;
 };
 
 constexpr int kMaxDev = 64;
@@ -437,48 +471,72 @@ int run_var_sorted(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d
 }
 
 // Arena path (crc32_arena.hip): one bulk pass over every line of [d_base, d_base + arena_bytes),
-// then one lane per payload. Scratch (c1, c8, c64: 73 words per 8 KiB superblock, ~3.6 % of the
+// then one lane per payload. Scratch (S quads, S_edge, SB: ~33 words per 1 KiB block, ~3.3 % of the
 // arena) comes from the stream-ordered allocator.
-int run_arena(DeviceCtx& c, const void* d_base, size_t arena_bytes, const uint64_t* d_off, const uint32_t* d_len,
-              size_t n, uint32_t* d_out, hipStream_t stream, bool update) {
-  ArenaLaunch a{};
+// Arena geometry and images for [d_base, d_base + arena_bytes) (everything but the batch and scratch).
+void arena_fill(const DeviceCtx& c, const void* d_base, size_t arena_bytes, ArenaLaunch& a) {
   a.base = d_base;
-  a.off = d_off;
-  a.len = d_len;
-  a.n = n;
-  a.out = d_out;
-  a.update = update;
   a.img_slice = c.d_slice;
   a.img_group8 = group_image(c, 8);
   a.img_sb = c.d_sb;
   a.img_stitch = c.d_stitch;
   a.zero_line = c.d_zero;
   a.max_blocks = (size_t)c.cus;
-  a.line_lo = 1;  // empty arena: every payload folds its lines directly
-  a.line_hi = 0;
-  uint32_t* scratch = nullptr;
-  if (arena_bytes) {
-    const uint64_t a0 = (uint64_t)(uintptr_t)d_base;
-    a.line_lo = a0 >> 7;
-    a.line_hi = (a0 + arena_bytes - 1) >> 7;
-    a.sb0 = a.line_lo >> 6;
-    a.nsb = (a.line_hi >> 6) - a.sb0 + 1;
-    a.fs0 = (a.line_lo + 63) >> 6;
-    a.fs1 = (a.line_hi + 1) >> 6;
-    if (a.fs1 < a.fs0) a.fs1 = a.fs0;
-    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&scratch), a.nsb * 73 * sizeof(uint32_t), stream));
-    a.c1 = scratch;
-    a.c8 = scratch + a.nsb * 64;
-    a.c64 = a.c8 + a.nsb * 8;
+  if (!arena_bytes) return;
+  a.byte_lo = (uint64_t)(uintptr_t)d_base;
+  a.byte_hi = a.byte_lo + arena_bytes;
+  a.line_lo = a.byte_lo >> 7;
+  a.line_hi = (a.byte_hi - 1) >> 7;
+  a.sb0 = a.line_lo >> 6;
+  a.nsb = (a.line_hi >> 6) - a.sb0 + 1;
+  a.fs0 = (a.byte_lo + 8191) >> 13;  // superblocks wholly inside the arena
+  a.fs1 = a.byte_hi >> 13;
+  if (a.fs1 < a.fs0) a.fs1 = a.fs0;
+}
+
+int run_arena(DeviceCtx& c, const void* d_base, size_t arena_bytes, const uint64_t* d_off, const uint32_t* d_len,
+              size_t n, uint32_t* d_out, hipStream_t stream, bool update) {
+  ArenaLaunch a{};
+  arena_fill(c, d_base, arena_bytes, a);
+  a.off = d_off;
+  a.len = d_len;
+  a.n = n;
+  a.out = d_out;
+  a.update = update;
+  if (!a.nsb) {
+    const hipError_t e = launch_arena(a, stream);
+    return e == hipSuccess ? ANNETY_CRC_OK : hip_fail(e);
   }
-  int rc = ANNETY_CRC_OK;
-  hipError_t e = launch_arena(a, stream);
-  if (e != hipSuccess) rc = hip_fail(e);
-  if (scratch) {
-    e = hipFreeAsync(scratch, stream);
-    if (rc == ANNETY_CRC_OK && e != hipSuccess) rc = hip_fail(e);
+  // scratch slot: the one this stream used last, else one whose last use has finished, else a new one,
+  // else slot 0 behind its event (the stream-ordered allocator cost ~3.6 us per call)
+  const size_t bytes = arena_geom(a).words * sizeof(uint32_t);
+  std::lock_guard<std::mutex> lk(c.arena_mu);
+  DeviceCtx::ScratchSlot* slot = nullptr;
+  for (int i = 0; i < c.arena_slots && !slot; i++)
+    if (c.arena_slot[i].last == stream) slot = &c.arena_slot[i];
+  for (int i = 0; i < c.arena_slots && !slot; i++)
+    if (hipEventQuery(c.arena_slot[i].done) == hipSuccess) slot = &c.arena_slot[i];
+  if (!slot && c.arena_slots < 8) {
+    DeviceCtx::ScratchSlot& fresh = c.arena_slot[c.arena_slots];
+    HIP_TRY(hipEventCreateWithFlags(&fresh.done, hipEventDisableTiming));
+    c.arena_slots++;
+    slot = &fresh;
   }
-  return rc;
+  if (!slot) slot = &c.arena_slot[0];
+  if (slot->last && slot->last != stream) HIP_TRY(hipStreamWaitEvent(stream, slot->done, 0));
+  if (slot->bytes < bytes) {
+    if (slot->ptr) HIP_TRY(hipFreeAsync(slot->ptr, stream));
+    slot->ptr = nullptr;
+    slot->bytes = 0;
+    HIP_TRY(hipMallocAsync(&slot->ptr, bytes, stream));
+    slot->bytes = bytes;
+  }
+  a.scratch = static_cast<uint32_t*>(slot->ptr);
+  const hipError_t e = launch_arena(a, stream);
+  const hipError_t r = hipEventRecord(slot->done, stream);
+  slot->last = stream;
+  if (e != hipSuccess) return hip_fail(e);
+  return r == hipSuccess ? ANNETY_CRC_OK : hip_fail(r);
 }
 
 bool fixed_fast_ok(const void* d_base, size_t len, size_t stride) {
@@ -635,6 +693,17 @@ int annety_crc_shutdown(void) {
       std::lock_guard<std::mutex> pl(c.pow_mu);
       for (auto& pw : c.powers) (void)hipFree(pw.second);
       c.powers.clear();
+    }
+    {
+      std::lock_guard<std::mutex> al(c.arena_mu);
+      for (int i = 0; i < c.arena_slots; i++) {
+        DeviceCtx::ScratchSlot& sl = c.arena_slot[i];
+        (void)hipEventSynchronize(sl.done);
+        if (sl.ptr) (void)hipFree(sl.ptr);
+        (void)hipEventDestroy(sl.done);
+        sl = DeviceCtx::ScratchSlot{};
+      }
+      c.arena_slots = 0;
     }
     c.d_slice = c.d_groups = nullptr;
     c.d_unshift = c.d_short = nullptr;

@@ -206,6 +206,23 @@ __device__ __forceinline__ uint4 gload16(uint64_t addr) {
   return make_uint4(x.x, x.y, x.z, x.w);
 }
 
+// Keep bytes [lo8/8, hi8/8) of a line (N = 8) or half line (N = 4), zero the rest (branch-free, per
+// 32-bit word).
+template <int N>
+__device__ __forceinline__ void mask_line(uint4 (&v)[N], int32_t lo8, int32_t hi8) {
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(&v[i]);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int32_t p8 = (i * 16 + q * 4) * 8;
+      const uint32_t keep_lo = (uint32_t)(0xFFFFFFFFull << clamp032(lo8 - p8));
+      const uint32_t keep_hi = (uint32_t)(0xFFFFFFFFull >> clamp032(p8 + 32 - hi8));
+      w[q] &= keep_lo & keep_hi;
+    }
+  }
+}
+
 // shift_{(7-g)*1024} for the leader lane of group g (k, v, g layout: conflict-free for the 8 leaders).
 __device__ __forceinline__ uint32_t sb_join(uint32_t s, const uint32_t* lds, uint32_t g) {
   const uint32_t* t = lds + kLdsSbJoinOff / 4 + g;

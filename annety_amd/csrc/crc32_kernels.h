@@ -65,26 +65,63 @@ hipError_t launch_split_desc(const void* base, size_t n, uint64_t len, uint64_t 
 hipError_t launch_split_join(const uint32_t* seg_crc, size_t n, uint32_t S, const uint32_t* powers, uint32_t* out,
                              hipStream_t stream);
 
-// Arena path (crc32_arena.hip): bulk line pass over [line_lo, line_hi] (absolute 128-byte lines,
-// superblocks of 64 lines from sb0, nsb of them; nsb = 0 skips the pass), then the per-payload stitch.
+// Arena path (crc32_arena.hip): bulk line pass over the arena [byte_lo, byte_hi) (absolute 128-byte
+// lines line_lo..line_hi, superblocks of 64 lines from sb0, nsb of them; nsb = 0 skips the pass), then
+// the per-payload stitch. DESIGN.md §2.8.
 struct ArenaLaunch {
   const void* base;          // payload offsets are relative to this pointer
-  uint64_t line_lo, line_hi; // arena lines (line_lo > line_hi: no arena, every payload folded directly)
+  uint64_t byte_lo, byte_hi; // the arena, absolute addresses (byte_lo == byte_hi: none, every payload folded directly)
+  uint64_t line_lo, line_hi; // its lines
   uint64_t sb0, nsb;         // superblocks (64 lines) overlapping the arena
-  uint64_t fs0, fs1;         // the full ones: [fs0, fs1), absolute superblock indices
+  uint64_t fs0, fs1;         // the ones wholly inside it: [fs0, fs1), absolute superblock indices
   const uint64_t* off;       // device, n entries
   const uint32_t* len;       // device, n entries
   size_t n;
-  uint32_t *c1, *c8, *c64;   // scratch: nsb*64, nsb*8, nsb words
+  uint32_t* scratch;         // arena_geom(*this).words words (device)
   const void* img_slice;     // common image part (slicing tables + half-line join)
   const void* img_group8;    // G = 8 group part (lane join + round maps)
   const void* img_sb;        // superblock join, kLdsSbJoinBytes
-  const void* img_stitch;    // level maps + inverse shifts, kLdsStitchImageBytes - kLdsCommonBytes
+  const void* img_stitch;    // stitch maps, kLdsStitchImageBytes - kLdsCommonBytes
   const void* zero_line;     // 128 zero bytes (device), read in place of lines outside the arena
   uint32_t* out;             // digests, or (update) registers in place
   size_t max_blocks;
   bool update;
 };
+
+// S of the full superblocks: kSTasks = 8 consecutive tasks of a wave leave together, as two 16-byte
+// stores per lane that each cover 1 KiB contiguously. Task t of lane-group `group`, line a, lives at word
+//   ((((t / 8) << (lg - 3)) + group / 8) * 2 + (t % 8) / 4) * 256 + ((group % 8) * 8 + a) * 4 + t % 4.
+constexpr uint32_t kSTasks = 8;
+inline __host__ __device__ uint64_t arena_s_word(uint64_t t, uint64_t group, uint32_t a, uint32_t lg) {
+  return (((((t >> 3) << (lg - 3)) + (group >> 3)) * 2 + ((t >> 2) & 1)) << 8) + (((group & 7) * 8 + a) << 2) +
+         (t & 3);
+}
+
+// Line-pass geometry: the grid (a power of two of 512-lane blocks, so lane-group and task of a block
+// are a mask and a shift), and the scratch layout [S bursts | SB nsb x 8 | S_edge 2 x 64] in words.
+struct ArenaGeom {
+  size_t blocks;      // line-pass workgroups
+  uint32_t lg;        // log2(lane-groups) = log2(blocks * 64)
+  uint64_t sb_off;    // word offset of SB (= words of the S bursts)
+  uint64_t edge_off;  // word offset of S_edge
+  uint64_t words;     // total
+};
+inline ArenaGeom arena_geom(const ArenaLaunch& a) {
+  ArenaGeom g{};
+  const uint64_t nblk = (a.fs1 - a.fs0) * 8;  // full 1 KiB blocks, one per lane-group task
+  uint64_t want = (nblk + 63) / 64;
+  if (want > a.max_blocks) want = a.max_blocks;
+  g.blocks = 1;
+  while (g.blocks * 2 <= want) g.blocks *= 2;
+  g.lg = 6;
+  while ((1ull << (g.lg - 6)) < g.blocks) g.lg++;
+  const uint64_t ngroups = (uint64_t)1 << g.lg;
+  const uint64_t bursts = ((nblk + ngroups - 1) / ngroups + kSTasks - 1) / kSTasks;
+  g.sb_off = bursts * ngroups * 8 * kSTasks;
+  g.edge_off = g.sb_off + a.nsb * 8;
+  g.words = g.edge_off + 128;
+  return g;
+}
 
 hipError_t launch_arena(const ArenaLaunch& a, hipStream_t stream);
 // the line pass alone (crc32_kernels.hip: the config-1 kernel in arena mode)

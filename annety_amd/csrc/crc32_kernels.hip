@@ -138,21 +138,28 @@ __global__ __launch_bounds__(kBlock) void crc32_fixed_kernel(const uint8_t* __re
 
 // Arena-mode arguments (crc32_arena.hip). The main loop streams the arena's FULL
 // superblocks [fs0, fs1) as 1 KiB blocks (base = superblock fs0, stride 1 KiB, G = 8); the partial
-// superblocks at the two ends, if any, are done first by global waves 0 and 1, whose lanes outside
-// [line_lo, line_hi] read the zero line.
+// superblocks at the two ends, if any, are done first by global waves 0 and 1, whose bytes outside the
+// arena [byte_lo, byte_hi) read as zeros (the zero line, or a byte mask on the two boundary lines).
+// Outputs, per line j of a 1 KiB block b: the suffix CRC S = raw(lines j..7 of b); per block g of a
+// superblock: SB = raw(blocks g..7 of the superblock). S of the full superblocks is stored in task-major
+// bursts (8 consecutive tasks together: arena_s_word in crc32_kernels.h), S of the partial ones in
+// S_edge[2][64]; SB as [superblock - sb0][g], one 32-byte store per superblock (in bursts from the 8
+// leader lanes the same bytes cost 11 us more: microbench/arena_mb.hip).
 struct ArenaOut {
-  uint32_t *c1, *c8, *c64;  // indexed from superblock sb0
-  uint64_t line_lo, line_hi, sb0, nsb, fs0, fs1;
+  uint32_t *S, *S_edge, *SB;
+  uint32_t lg;  // log2(lane-groups of the grid)
+  uint64_t byte_lo, byte_hi, line_lo, line_hi, sb0, nsb, fs0, fs1;
   uint64_t zero_line;
 };
 
 // Single-round fast path (payload = exactly G lines, 16-byte aligned; BASELINE config 1 is G = 8):
 // each step is one whole payload per lane-group, so there is no round state, and the per-lane line
 // pointer advances by a constant per task. Loads run one task ahead (A/B double buffer).
-//   ARENA (G = 8): the arena line pass instead of digests - per line the raw CRC c1 (register 0, no
-//   init), per 1 KiB block the join c8, per 8 KiB superblock (the 8 groups of a wave) c64.
-//   PROBE (microbench only; product = 0, ARENA only): bit 0 drops the c1 store, bit 1 the superblock
-//   join - wrong outputs, used to measure what those stages cost.
+//   ARENA (G = 8): the arena line pass instead of digests (ArenaOut above): per line the raw CRC
+//   (register 0, no init) mapped to its block end, the block's suffix scan S, and across the 8 groups of
+//   a wave (one superblock) the suffix scan SB.
+//   PROBE (microbench only; product = 0, ARENA only): bit 0 drops the S store, bit 1 the superblock
+//   scan - wrong outputs, used to measure what those stages cost.
 template <int G, int BLK = kBlock, int VWG = kVwg, bool ARENA = false, int PROBE = 0>
 __global__ __launch_bounds__(BLK) void crc32_oneround_kernel(const uint8_t* __restrict__ base, size_t n,
                                                                 size_t stride, const uint4* __restrict__ img_slice,
@@ -187,24 +194,40 @@ __global__ __launch_bounds__(BLK) void crc32_oneround_kernel(const uint8_t* __re
   __syncthreads();
 
   const uint32_t lane = threadIdx.x & 63;
-  // arena mode: block index (relative to superblock sb0) of this group's current task
-  uint64_t blk = ARENA ? (ar.fs0 - ar.sb0) * 8 + gid : 0;
-  // Interleaved with the read stream, each written byte costs about five read bytes: the c1 array (3 %
-  // of the arena) costs ~14 % of the pass (microbench/arena_mb.hip).
-  auto arena_out = [&](uint32_t r, uint64_t b) {  // r = raw CRC of this lane's line, b = its block
-    if constexpr ((PROBE & 1) == 0) __builtin_nontemporal_store(r, ar.c1 + b * 8 + j);
-    const uint32_t t = group_xor_reduce<8>(nibble_map_lane(r, lds, k.slot4));  // complete on j == 7
-    uint32_t u = 0;
-    if (j == 7) {
-      ar.c8[b] = t;
-      if constexpr ((PROBE & 2) == 0) u = sb_join(t, lds, lane >> 3);
-    }
+  // S of 8 consecutive tasks leaves in two 16-byte nontemporal stores per lane, each 1 KiB contiguous
+  // per wave: interleaved with the read stream, a dword per lane per task cost 30 us of a 211 us pass,
+  // 16-byte quads of 4 tasks 20 (microbench/arena_mb.hip).
+  uint32_t q[kSTasks];
+#pragma unroll
+  for (uint32_t i = 0; i < kSTasks; i++) q[i] = 0;
+  // r = raw CRC of this lane's line, b = its block (relative to sb0); returns S for this lane's line
+  // r = raw CRC of this lane's line; returns S for it and (lanes j == 0) SB for its block
+  auto arena_scan = [&](uint32_t r, uint32_t& sbv) {
+    uint32_t x = nibble_map_lane(r, lds, k.slot4);  // shift_{(7-j)*128}(r): the line seen from the block end
+    // suffix scan over the 8 lanes of the group (DPP row_shl:d = the value of lane + d in its row of 16)
+    uint32_t y;
+    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x101, 0xF, 0xF, false);
+    x ^= j + 1 < 8 ? y : 0u;
+    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x102, 0xF, 0xF, false);
+    x ^= j + 2 < 8 ? y : 0u;
+    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x104, 0xF, 0xF, false);
+    x ^= j + 4 < 8 ? y : 0u;  // S: lines j..7
+    sbv = 0;
     if constexpr ((PROBE & 2) == 0) {
-      u ^= __shfl_xor(u, 8, 64);
-      u ^= __shfl_xor(u, 16, 64);
-      u ^= __shfl_xor(u, 32, 64);
-      if (lane == 63) ar.c64[b >> 3] = u;
+      // the 8 groups of a wave are one superblock, in order (g = lane / 8): block g seen from the
+      // superblock end on lane 8g, then the suffix scan of those 8 values in scalar registers
+      const uint32_t g = lane >> 3;
+      uint32_t u = 0;
+      if (j == 0) u = sb_join(x, lds, g);
+      uint32_t t[8];
+      t[7] = (uint32_t)__builtin_amdgcn_readlane((int)u, 56);
+#pragma unroll
+      for (int h = 6; h >= 0; h--) t[h] = t[h + 1] ^ (uint32_t)__builtin_amdgcn_readlane((int)u, 8 * h);
+      sbv = t[0];
+#pragma unroll
+      for (uint32_t h = 1; h < 8; h++) sbv = g == h ? t[h] : sbv;  // SB: blocks g..7
     }
+    return x;
   };
   if constexpr (ARENA) {
     // partial superblocks at the arena ends (wave-uniform, two waves of the grid)
@@ -213,23 +236,45 @@ __global__ __launch_bounds__(BLK) void crc32_oneround_kernel(const uint8_t* __re
       const uint64_t sb = gw == 0 ? ar.sb0 : ar.sb0 + ar.nsb - 1;
       if ((sb < ar.fs0 || sb >= ar.fs1) && (gw == 0 || sb != ar.sb0)) {
         const uint64_t line = sb * 64 + lane;
-        const uint64_t src = line >= ar.line_lo && line <= ar.line_hi ? line << 7 : ar.zero_line;
+        const bool in = line >= ar.line_lo && line <= ar.line_hi;
+        const uint64_t src = in ? line << 7 : ar.zero_line;
         uint4 v[8];
 #pragma unroll
         for (int i = 0; i < 8; i++) v[i] = gload16(src + 16 * i);
-        arena_out(absorb_line(0u, v, k, lds), (sb - ar.sb0) * 8 + (lane >> 3));
+        const int32_t lo8 = line == ar.line_lo ? (int32_t)(ar.byte_lo & 127) * 8 : 0;
+        const int32_t hi8 = line == ar.line_hi ? (int32_t)(((ar.byte_hi - 1) & 127) + 1) * 8 : 1024;
+        mask_line(v, lo8, hi8);
+        uint32_t sbv;
+        const uint32_t x = arena_scan(absorb_line(0u, v, k, lds), sbv);
+        if constexpr ((PROBE & 1) == 0) ar.S_edge[gw * 64 + lane] = x;
+        if (j == 0) ar.SB[(sb - ar.sb0) * 8 + (lane >> 3)] = sbv;
       }
     }
   }
 
-  auto finish = [&](uint32_t s) {
+  auto finish = [&](uint32_t s, int t) {
     if constexpr (ARENA) {
-      arena_out(s, blk);
-      blk += ngroups;
+      uint32_t sbv;
+      const uint32_t x = arena_scan(s, sbv);
+      const uint32_t slot = (uint32_t)t & (kSTasks - 1);
+#pragma unroll
+      for (uint32_t i = 0; i < kSTasks; i++) q[i] = slot == i ? x : q[i];
+      if constexpr ((PROBE & 2) == 0) {
+        if (j == 0) ar.SB[(ar.fs0 - ar.sb0 + (((uint64_t)t << ar.lg) + gid) / 8) * 8 + (lane >> 3)] = sbv;
+      }
+      if (slot == kSTasks - 1 || t + 1 == ntasks) {
+        const uint64_t t0 = (uint64_t)t & ~7ull;
+        if constexpr ((PROBE & 1) == 0) {
+          v4u32* dst = reinterpret_cast<v4u32*>(ar.S + arena_s_word(t0, gid, j, ar.lg));
+          const v4u32 lo = {q[0], q[1], q[2], q[3]}, hi = {q[4], q[5], q[6], q[7]};
+          __builtin_nontemporal_store(lo, dst);
+          __builtin_nontemporal_store(hi, dst + 64);  // + 1 KiB
+        }
+      }
     } else {
-      uint32_t t = s;
-      if constexpr (G > 1) t = group_xor_reduce<G>(nibble_map_lane(s, lds, k.slot4));
-      if (j == G - 1) *op = ~t;
+      uint32_t u = s;
+      if constexpr (G > 1) u = group_xor_reduce<G>(nibble_map_lane(s, lds, k.slot4));
+      if (j == G - 1) *op = ~u;
       op += ngroups;
     }
   };
@@ -243,14 +288,14 @@ __global__ __launch_bounds__(BLK) void crc32_oneround_kernel(const uint8_t* __re
       for (int i = 0; i < 8; i++) B[i] = s[i];
     }
     __builtin_amdgcn_sched_barrier(0);
-    finish(absorb_line(sinit, A, k, lds));
+    finish(absorb_line(sinit, A, k, lds), t);
     {
       const uint4* s = reinterpret_cast<const uint4*>(t + 2 < ntasks ? lp + 2 * pstep : lp);
 #pragma unroll
       for (int i = 0; i < 8; i++) A[i] = s[i];
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (t + 1 < ntasks) finish(absorb_line(sinit, B, k, lds));
+    if (t + 1 < ntasks) finish(absorb_line(sinit, B, k, lds), t + 1);
     lp += 2 * pstep;
   }
 }
@@ -714,10 +759,14 @@ hipError_t launch_full(const FixedLaunch& a, hipStream_t stream) {
 
 template <int PROBE>
 hipError_t launch_arena_lines_p(const ArenaLaunch& a, hipStream_t stream) {
+  const ArenaGeom geo = arena_geom(a);
   ArenaOut ar;
-  ar.c1 = a.c1;
-  ar.c8 = a.c8;
-  ar.c64 = a.c64;
+  ar.S = a.scratch;
+  ar.SB = a.scratch + geo.sb_off;
+  ar.S_edge = a.scratch + geo.edge_off;
+  ar.lg = geo.lg;
+  ar.byte_lo = a.byte_lo;
+  ar.byte_hi = a.byte_hi;
   ar.line_lo = a.line_lo;
   ar.line_hi = a.line_hi;
   ar.sb0 = a.sb0;
@@ -725,10 +774,10 @@ hipError_t launch_arena_lines_p(const ArenaLaunch& a, hipStream_t stream) {
   ar.fs0 = a.fs0;
   ar.fs1 = a.fs1;
   ar.zero_line = (uint64_t)(uintptr_t)a.zero_line;
+  static_assert(kBlock / 8 == 64 && kSTasks == 8, "arena_geom / arena_s_word assume 64 groups per block, 8-task bursts");
   const size_t nblk = (size_t)(a.fs1 - a.fs0) * 8;  // full 1 KiB blocks
-  const size_t blocks = std::max<size_t>(1, std::min<size_t>(a.max_blocks, (nblk * 8 + kBlock - 1) / kBlock));
-  hipLaunchKernelGGL((crc32_oneround_kernel<8, kBlock, kVwg, true, PROBE>), dim3((unsigned)blocks), dim3(kBlock), 0,
-                     stream, reinterpret_cast<const uint8_t*>((uintptr_t)(a.fs0 * 8192)), nblk, (size_t)1024,
+  hipLaunchKernelGGL((crc32_oneround_kernel<8, kBlock, kVwg, true, PROBE>), dim3((unsigned)geo.blocks), dim3(kBlock),
+                     0, stream, reinterpret_cast<const uint8_t*>((uintptr_t)(a.fs0 * 8192)), nblk, (size_t)1024,
                      static_cast<const uint4*>(a.img_slice), static_cast<const uint4*>(a.img_group8), nullptr,
                      static_cast<const uint4*>(a.img_sb), ar);
   return hipGetLastError();

@@ -115,12 +115,18 @@ constexpr uint32_t kChunkBytes = 128;  // one cache line per lane per round
 constexpr uint32_t kLdsSbJoinOff = kLdsImageBytes;
 constexpr uint32_t kLdsSbJoinBytes = 4096;
 constexpr uint32_t kLdsArenaImageBytes = kLdsSbJoinOff + kLdsSbJoinBytes;  // 152576
-// Arena path, stitch kernel: common + level maps + inverse shifts (no group part)
-//   [kLdsCommonBytes, +1.5 KiB)  level L = 0/1/2: (k, v) at L*512 + k*64 + v*4 = shift_{128*8^L}(v << 4k)
-//   [+1.5 KiB, +12 KiB)          U_lo[m] = shift_{-m}, U_hi[h] = shift_{-16h} (same layout as kLdsUnshiftOff)
-constexpr uint32_t kLdsLevelOff = kLdsCommonBytes;
-constexpr uint32_t kLdsLevelBytes = 3 * 512;
-constexpr uint32_t kLdsStitchUnshiftOff = kLdsLevelOff + kLdsLevelBytes;
-constexpr uint32_t kLdsStitchImageBytes = kLdsStitchUnshiftOff + kLdsUnshiftBytes;  // 145408
+// Arena path, stitch kernel: common + segment maps + inverse shifts + quarter-line join (no group part)
+//   [kLdsMapOff, +16 KiB)  set of 32 maps, (k, i, v) at (k*32 + i)*64 + v*4: i = m-1: F(m) = shift_{128m}
+//                          (m = 1..8), 7+m: G(m) = shift_{1024m}, 16+q: UL(q) = shift_{-128q},
+//                          24+q: UB(q) = shift_{-1024q} (q = 0..7)
+//   [kLdsStitchUnshiftOff, +8 KiB)  set U_lo[m] = shift_{-m}, (k, m, v) at (k*16 + m)*64 + v*4
+//   [+8 KiB, +12 KiB)                set U_hi[h] = shift_{-16h}, (k, h, v) at (k*8 + h)*64 + v*4
+//   [kLdsQuarterOff, +512)  shift_32 (joins the two 32-byte chains of a half-line window)
+constexpr uint32_t kLdsMapOff = kLdsCommonBytes;
+constexpr uint32_t kLdsMapBytes = 32 * 512;
+constexpr uint32_t kMapF = 0, kMapG = 8, kMapUL = 16, kMapUB = 24;  // map index of F(1), G(1), UL(0), UB(0)
+constexpr uint32_t kLdsStitchUnshiftOff = kLdsMapOff + kLdsMapBytes;
+constexpr uint32_t kLdsQuarterOff = kLdsStitchUnshiftOff + kLdsUnshiftBytes;
+constexpr uint32_t kLdsStitchImageBytes = kLdsQuarterOff + 512;  // 160768 <= 163840
 
 }  // namespace annety_crc

@@ -1,5 +1,5 @@
 // Arena line pass breakdown at config-3 size (1 GiB arena): the product kernel vs PROBE variants that
-// drop the c1 store / superblock join / block join, next to the config-1 kernel on the same bytes.
+// drop the S store / superblock scan, next to the config-1 kernel on the same bytes.
 #include "../annety_amd/csrc/crc32_kernels.hip"
 #include "../annety_amd/csrc/crc32_arena.hip"
 #include "../annety_amd/csrc/crc32_frames.hip"
@@ -11,9 +11,7 @@
 using namespace annety_crc;
 
 template <int PROBE>
-void lines(DeviceCtx& c, ArenaLaunch a) {
-  a.img_slice = c.d_slice; a.img_group8 = group_image(c, 8); a.img_sb = c.d_sb; a.zero_line = c.d_zero;
-  a.max_blocks = c.cus;
+void lines(DeviceCtx&, const ArenaLaunch& a) {
   CK(launch_arena_lines_p<PROBE>(a, 0));
 }
 
@@ -25,11 +23,9 @@ int main() {
   RC(annety_crc_init(0));
   DeviceCtx* c = nullptr; RC(current_ctx(&c));
   ArenaLaunch a{};
-  a.line_lo = (uint64_t)(uintptr_t)d >> 7; a.line_hi = ((uint64_t)(uintptr_t)d + bytes - 1) >> 7;
-  a.sb0 = a.line_lo >> 6; a.nsb = (a.line_hi >> 6) - a.sb0 + 1;
-  a.fs0 = (a.line_lo + 63) >> 6; a.fs1 = (a.line_hi + 1) >> 6;
-  CK(hipMalloc(&scratch, a.nsb * 73 * 4)); CK(hipMalloc(&out, (bytes / 1024) * 4));
-  a.c1 = scratch; a.c8 = scratch + a.nsb * 64; a.c64 = a.c8 + a.nsb * 8;
+  arena_fill(*c, d, bytes, a);
+  CK(hipMalloc(&scratch, arena_geom(a).words * 4)); CK(hipMalloc(&out, (bytes / 1024) * 4));
+  a.scratch = scratch;
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   auto t = [&](auto f, const char* name) {
     for (int w = 0; w < 200; w++) f();
@@ -42,10 +38,10 @@ int main() {
   };
   t([&] { RC(annety_crc32_batch_fixed(d, bytes / 1024, 1024, 1024, out, nullptr)); }, "config-1 kernel (oneround<8>)");
   t([&] { lines<0>(*c, a); }, "arena lines (product)");
-  t([&] { lines<1>(*c, a); }, "  no c1 store");
-  t([&] { lines<2>(*c, a); }, "  no superblock join");
-  t([&] { lines<3>(*c, a); }, "  no c1 store, no sb join");
-  // c1 traffic alone: the same 32 MiB of stores as a separate pass
-  t([&] { CK(hipMemsetAsync(a.c1, 0, a.nsb * 64 * 4, 0)); }, "memset of c1 (32 MiB)");
+  t([&] { lines<1>(*c, a); }, "  no S store");
+  t([&] { lines<2>(*c, a); }, "  no superblock scan");
+  t([&] { lines<3>(*c, a); }, "  no S store, no superblock scan");
+  // S traffic alone: the same 32 MiB of stores as a separate pass
+  t([&] { CK(hipMemsetAsync(a.scratch, 0, a.nsb * 64 * 4, 0)); }, "memset of S (32 MiB)");
   return 0;
 }

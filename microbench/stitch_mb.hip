@@ -1,5 +1,5 @@
 // Arena stitch breakdown on the config-3 batch (Zipf lengths as bench.py, packed, ~1 GiB): the full
-// stitch vs PROBE variants (descriptors only / + edge loads / + edge folds), after one real line pass.
+// stitch vs PROBE variants (descriptors only / + all loads / + window folds), after one real line pass.
 #include "../annety_amd/csrc/crc32_kernels.hip"
 #include "../annety_amd/csrc/crc32_arena.hip"
 #include "../annety_amd/csrc/crc32_frames.hip"
@@ -12,13 +12,6 @@
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__); exit(1);} } while (0)
 #define RC(x) do { int r_ = (x); if (r_) { printf("%s -> %d\n", #x, r_); exit(3); } } while (0)
 using namespace annety_crc;
-
-template <int PROBE>
-void stitch(const ArenaLaunch& a) {
-  hipLaunchKernelGGL((crc32_arena_stitch_kernel<false, kStitchBlock, PROBE>), dim3((unsigned)stitch_blocks(a)),
-                     dim3(kStitchBlock), 0, 0, (const uint8_t*)a.base, a.line_lo, a.line_hi, a.sb0, a.off, a.len, a.n,
-                     a.c1, a.c8, a.c64, (const uint4*)a.img_slice, (const uint4*)a.img_stitch, a.out);
-}
 
 int main() {
   setvbuf(stdout, nullptr, _IOLBF, 0);
@@ -48,14 +41,9 @@ int main() {
   RC(annety_crc_init(0));
   DeviceCtx* c = nullptr; RC(current_ctx(&c));
   ArenaLaunch a{};
-  a.base = d; a.off = doff; a.len = dlen; a.n = n; a.out = out;
-  a.img_slice = c->d_slice; a.img_group8 = group_image(*c, 8); a.img_sb = c->d_sb; a.img_stitch = c->d_stitch;
-  a.zero_line = c->d_zero; a.max_blocks = c->cus;
-  const uint64_t a0 = (uint64_t)(uintptr_t)d;
-  a.line_lo = a0 >> 7; a.line_hi = (a0 + total - 1) >> 7; a.sb0 = a.line_lo >> 6; a.nsb = (a.line_hi >> 6) - a.sb0 + 1;
-  a.fs0 = (a.line_lo + 63) >> 6; a.fs1 = (a.line_hi + 1) >> 6;
-  uint32_t* scratch; CK(hipMalloc(&scratch, a.nsb * 73 * 4));
-  a.c1 = scratch; a.c8 = scratch + a.nsb * 64; a.c64 = a.c8 + a.nsb * 8;
+  arena_fill(*c, d, total, a);
+  a.off = doff; a.len = dlen; a.n = n; a.out = out;
+  CK(hipMalloc(&a.scratch, arena_geom(a).words * 4));
   CK(launch_arena_lines(a, 0));
   CK(hipDeviceSynchronize());
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
@@ -69,11 +57,11 @@ int main() {
     printf("%-40s %.2f us\n", name, ms / 100 * 1000);
   };
   t([&] { CK(launch_arena_lines(a, 0)); }, "line pass");
-  t([&] { stitch<0>(a); }, "stitch (product)");
-  t([&] { stitch<1>(a); }, "  descriptors + store only");
-  t([&] { stitch<2>(a); }, "  + edge line loads");
-  t([&] { stitch<3>(a); }, "  + edge folds, no interior steps");
-  t([&] { stitch<4>(a); }, "stitch with two single-line folds");
+  t([&] { CK(launch_stitch_p<0>(a, 0)); }, "stitch (product)");
+  t([&] { CK(launch_stitch_p<1>(a, 0)); }, "  descriptors + store only");
+  t([&] { CK(launch_stitch_p<2>(a, 0)); }, "  + all loads");
+  t([&] { CK(launch_stitch_p<3>(a, 0)); }, "  + window folds, no map steps");
+  t([&] { CK(launch_arena(a, 0)); }, "line pass + stitch (no alloc)");
   t([&] { RC(annety_crc32_batch_var_arena(d, total, doff, dlen, n, out, nullptr)); }, "product arena call (both + alloc)");
   return 0;
 }

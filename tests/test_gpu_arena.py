@@ -145,3 +145,42 @@ def test_arena_streaming_fragments(gpu):
     got = u32(sc.digests())
     want = np.array([oracle.crc32_long(b) for b in bodies], dtype=np.uint32)
     assert np.array_equal(got, want)
+
+
+def test_arena_partial_ends(gpu):
+    """Arenas that start and end mid-line and mid-superblock, with nonzero bytes around them in the
+    same lines: payloads touching the first and last arena byte, every start/end offset within the
+    boundary lines, arenas inside one line, one superblock and across two (no whole superblock)."""
+    import annety_amd
+
+    rng = np.random.default_rng(21)
+    host = oracle.lcg_bytes(3 << 20, 5)
+    d = to_dev(host, gpu)
+    for lo, size in ((37, 90), (5, 200), (8100, 300), (8190, 8200), (40, 16384 + 1000), (4096 + 77, (1 << 20) + 333),
+                     (8192, 65536), (8192 + 64, (2 << 20) - 8192 - 64 - 13)):
+        sub = d[lo:lo + size]
+        offs, lens = [], []
+        for a in range(0, min(size, 160)):  # starts in the first lines, ends anywhere
+            offs.append(a)
+            lens.append(int(rng.integers(0, size - a + 1)))
+        for e in range(max(0, size - 160), size + 1):  # ends in the last lines
+            a = int(rng.integers(0, e + 1))
+            offs.append(a)
+            lens.append(e - a)
+        offs.append(0)
+        lens.append(size)
+        for _ in range(400):
+            a = int(rng.integers(0, size))
+            offs.append(a)
+            lens.append(int(rng.integers(0, size - a + 1)))
+        offs = np.array(offs, np.int64)
+        lens = np.array(lens, np.int64)
+        want = oracle.batch_var_mt(host[lo:lo + size], offs, lens, 8)
+        got = u32(annety_amd.crc32_batch_var(sub, to_dev(offs, gpu), to_dev(lens.astype(np.int32), gpu), arena=True))
+        bad = np.nonzero(got != want)[0]
+        assert bad.size == 0, (lo, size, offs[bad[:4]], lens[bad[:4]])
+        st = rng.integers(0, 2 ** 32, offs.size, dtype=np.uint64).astype(np.uint32)
+        d_state = to_dev(st.view(np.int32), gpu)
+        annety_amd.crc32_update_batch_var(d_state, sub, to_dev(offs, gpu), to_dev(lens.astype(np.int32), gpu),
+                                          arena=True)
+        assert np.array_equal(u32(d_state), oracle.batch_var_mt(host[lo:lo + size], offs, lens, 8, states=st)), (lo, size)
