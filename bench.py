@@ -37,7 +37,7 @@ sys.path.insert(0, ROOT)
 METRIC = "CRC-32C GiB/s device-resident (1M×1KiB) @1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md (8.0 TB/s)
 # Per-launch HBM bytes measured by profiles/pmc.sh at this code (FETCH_SIZE x2 + WRITE_SIZE), per config.
-PMC_FILES = {1: "profiles/r02/config1_pmc.json", 3: "profiles/r02/config3_arena_pmc.json",
+PMC_FILES = {1: "profiles/r02/config1_pmc.json", 3: "profiles/r02/config3_pmc.json",
              2: "profiles/r02/config2_pmc.json", 4: "profiles/r02/config1_pmc.json"}
 # The reference build of oracle/_ref (oracle/Makefile): the reference's Release flags without -march=native.
 REF_FLAGS = "g++ -std=c++11 -O2 -DNDEBUG (CMakeLists.txt:24,48 Release flags; -march=native dropped so the .so runs on any host)"
