@@ -32,6 +32,7 @@
 
 #include <algorithm>
 
+#include "crc32_arena_lines.h"
 #include "crc32_device.h"
 #include "crc32_kernels.h"
 #include "crc32_math.h"
@@ -86,16 +87,16 @@ __device__ __forceinline__ void absorb_two_windows(const uint4 (&v)[4], const ui
   rw = nibble_map_uniform(xc, lds, kLdsQuarterOff) ^ xd;
 }
 
-struct StitchArgs {
+// Where the stitch finds a call's batch and the line pass's outputs (layout: crc32_kernels.h).
+struct StitchGeo {
   const uint8_t* base;
   uint64_t byte_lo, byte_hi, line_lo, line_hi, sb0, fs0, fs1;
-  uint32_t lg;
-  const uint32_t *S, *SB, *S_edge;
+  uint64_t W;   // line-pass waves = 8 * L
+  uint32_t L;   // line-pass workgroups (64 L lane groups)
+  const uint32_t *S, *SB, *S_edge, *SB_edge;
   const uint64_t* off;
   const uint32_t* len;
   size_t n;
-  const uint4* img_slice;
-  const uint4* img_stitch;
   uint64_t zero_line;
   uint32_t* out;
 };
@@ -112,6 +113,7 @@ struct Plan {
   uint32_t act, yzero;          // per step bit: active / second operand is zero
   uint32_t nmid;
   uint64_t mid_s;               // first whole superblock between (relative to sb0)
+  uint64_t xa[4], ya[4];        // step operand addresses
 };
 struct Vals {
   uint4 h[4], t[4];
@@ -119,38 +121,41 @@ struct Vals {
   uint32_t s0;
 };
 
+// The per-payload stitch (file comment). Phase A issues everything the line pass did not write, phase
+// B the S/SB words.
 //   PROBE (microbench only; product = 0): 1 = descriptors and stores only, 2 = + all loads,
 //   3 = + window folds (no map steps) - wrong digests, used to measure what the stages cost.
-template <bool UPD, int BLK = kStitchBlock, int PROBE = 0>
-__global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchArgs g) {
-  __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsStitchImageBytes / 16];
-  const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
+template <bool UPD, int PROBE>
+struct Stitcher {
+  const StitchGeo& g;
+  const uint32_t* lds;
   LaneCtx k;
-  k.L0 = (threadIdx.x & 31) << 3;
-  k.L1 = k.L0 | (1u << 16);
-  k.slot4 = (threadIdx.x & 31) << 2;
-  const uint64_t gmask = ((uint64_t)1 << g.lg) - 1;
-  const uint64_t s_base = (uint64_t)(uintptr_t)g.S, e_base = (uint64_t)(uintptr_t)g.S_edge;
-  const uint64_t sb_base = (uint64_t)(uintptr_t)g.SB;
 
-  // address of S for line a (0..7) of block rb (relative to superblock sb0): task-major bursts for the
-  // full superblocks (crc32_kernels.h kSTasks), S_edge for the partial ones
-  auto s_addr = [&](uint64_t rb, uint32_t a) -> uint64_t {
+  __device__ __forceinline__ uint32_t word(uint64_t addr) const { return gload4(addr); }
+  // address of S for line a (0..7) of block rb (relative to superblock sb0)
+  __device__ __forceinline__ uint64_t s_addr(uint64_t rb, uint32_t a) const {
     const uint64_t sb = g.sb0 + (rb >> 3);
     const bool edge = sb < g.fs0 || sb >= g.fs1;
-    const uint64_t r = rb - (g.fs0 - g.sb0) * 8;
-    const uint64_t t = r >> g.lg;
-    const uint64_t burst = arena_s_word(t, r & gmask, a, g.lg) * 4;
+    const uint32_t r = (uint32_t)(rb - (g.fs0 - g.sb0) * 8);  // block of the full range (< 2^32: host check)
+    const uint32_t t = (r >> 6) / g.L;                        // task; lane group = r - t * 64 L
+    const uint64_t full = arena_s_word(t, r - t * 64 * g.L, a, g.W) * 4;
     const uint64_t ed = ((sb == g.sb0 ? 0 : 64) + (rb & 7) * 8 + a) * 4;
-    return edge ? e_base + ed : s_base + burst;
-  };
-  auto sb_addr = [&](uint64_t sbr, uint32_t gg) -> uint64_t { return sb_base + (sbr * 8 + gg) * 4; };
+    return edge ? (uint64_t)(uintptr_t)g.S_edge + ed : (uint64_t)(uintptr_t)g.S + full;
+  }
+  // address of SB for block gg of superblock sbr (relative to sb0)
+  __device__ __forceinline__ uint64_t sb_addr(uint64_t sbr, uint32_t gg) const {
+    const uint64_t sb = g.sb0 + sbr;
+    const bool edge = sb < g.fs0 || sb >= g.fs1;
+    const uint64_t full = ((sb - g.fs0) * 8 + gg) * 4;
+    const uint64_t ed = ((sb == g.sb0 ? 0 : 8) + gg) * 4;
+    return edge ? (uint64_t)(uintptr_t)g.SB_edge + ed : (uint64_t)(uintptr_t)g.SB + full;
+  }
 
-  auto plan_and_load = [&](size_t p, Plan& y, Vals& v) {
+  // Phase A: descriptor, plan, window and register loads (nothing the line pass writes).
+  __device__ __forceinline__ void plan_a(size_t p, Plan& y, Vals& v) const {
     y.len = g.len[p];
     y.A = (uint64_t)(uintptr_t)g.base + g.off[p];
     y.E = y.A + y.len;
-    const uint64_t dummy = (uint64_t)(uintptr_t)(g.len + p);
     y.fast = y.len > 0 && y.A >= g.byte_lo && y.E <= g.byte_hi;
     const uint64_t L0 = y.A >> 7, L1 = (y.E - (y.len ? 1 : 0)) >> 7;
     y.lead = (uint32_t)(y.A & 127);
@@ -174,6 +179,7 @@ __global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchArgs g) {
     for (int i = 0; i < 4; i++) v.h[i] = gload16(hsrc + 16 * i);
 #pragma unroll
     for (int i = 0; i < 4; i++) v.t[i] = gload16(tsrc + 16 * i);
+    v.s0 = UPD ? gload4((uint64_t)(uintptr_t)(g.out + p)) : kInit;
 
     // whole lines I0..I1 (empty when I1 < I0)
     const int64_t I0 = (int64_t)L0 + (y.headX ? 0 : 1), I1 = (int64_t)L1 - (y.tailX ? 0 : 1);
@@ -187,47 +193,50 @@ __global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchArgs g) {
     const uint64_t s0 = B0 >> 3, s1 = B1 >> 3;
     const uint32_t g0 = (uint32_t)B0 & 7, g1 = (uint32_t)B1 & 7;
     const bool one = s0 == s1;
-    uint64_t xa[4], ya[4];
     // step 0: head block (or the whole run when it stays in one block)
     y.m1[0] = kMapF + (same ? z - a + 1 : 8 - a) - 1;
     y.m2[0] = kMapUL + (same ? 7 - z : 0);
-    xa[0] = s_addr(rb0, a);
-    ya[0] = s_addr(rb0, z + 1 < 8 ? z + 1 : 0);
-    bool yz0 = !same || z == 7;
+    y.xa[0] = s_addr(rb0, a);
+    y.ya[0] = s_addr(rb0, z + 1 < 8 ? z + 1 : 0);
+    const bool yz0 = !same || z == 7;
     // step 1: blocks of the first partial superblock (or all of them when they stay in one)
     y.m1[1] = kMapG + (one ? g1 - g0 + 1 : 8 - g0) - 1;
     y.m2[1] = kMapUB + (one ? 7 - g1 : 0);
-    xa[1] = sb_addr(s0, g0);
-    ya[1] = sb_addr(s0, g1 + 1 < 8 ? g1 + 1 : 0);
-    bool yz1 = !one || g1 == 7;
+    y.xa[1] = sb_addr(s0, g0);
+    y.ya[1] = sb_addr(s0, g1 + 1 < 8 ? g1 + 1 : 0);
+    const bool yz1 = !one || g1 == 7;
     // step 2: blocks 0..g1 of the last partial superblock
     y.m1[2] = kMapG + g1;
     y.m2[2] = kMapUB + (7 - g1);
-    xa[2] = sb_addr(s1, 0);
-    ya[2] = sb_addr(s1, g1 + 1 < 8 ? g1 + 1 : 0);
-    bool yz2 = g1 == 7;
+    y.xa[2] = sb_addr(s1, 0);
+    y.ya[2] = sb_addr(s1, g1 + 1 < 8 ? g1 + 1 : 0);
+    const bool yz2 = g1 == 7;
     // step 3: lines 0..z of the tail block
     y.m1[3] = kMapF + z;
     y.m2[3] = kMapUL + (7 - z);
-    xa[3] = s_addr(rb1, 0);
-    ya[3] = s_addr(rb1, z + 1 < 8 ? z + 1 : 0);
-    bool yz3 = z == 7;
+    y.xa[3] = s_addr(rb1, 0);
+    y.ya[3] = s_addr(rb1, z + 1 < 8 ? z + 1 : 0);
+    const bool yz3 = z == 7;
     y.act = (seg ? 1u : 0u) | (blocks ? 2u : 0u) | (blocks && !one ? 4u : 0u) | (seg && !same ? 8u : 0u);
     y.yzero = (yz0 ? 1u : 0u) | (yz1 ? 2u : 0u) | (yz2 ? 4u : 0u) | (yz3 ? 8u : 0u);
     y.nmid = blocks && !one ? (uint32_t)(s1 - s0 - 1) : 0u;
     y.mid_s = s0 + 1;
+  }
+
+  // Phase B: the S/SB words of the plan.
+  __device__ __forceinline__ void plan_b(size_t p, const Plan& y, Vals& v) const {
+    const uint64_t dummy = (uint64_t)(uintptr_t)(g.len + p);
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       const bool on = (y.act >> q) & 1u;
-      v.x[q] = gload4(on ? xa[q] : dummy);
-      v.y[q] = gload4(on && !((y.yzero >> q) & 1u) ? ya[q] : dummy);
+      v.x[q] = word(on ? y.xa[q] : dummy);
+      v.y[q] = word(on && !((y.yzero >> q) & 1u) ? y.ya[q] : dummy);
     }
 #pragma unroll
-    for (int q = 0; q < 8; q++) v.mid[q] = gload4((uint32_t)q < y.nmid ? sb_addr(y.mid_s + q, 0) : dummy);
-    v.s0 = UPD ? gload4((uint64_t)(uintptr_t)(g.out + p)) : kInit;
-  };
+    for (int q = 0; q < 8; q++) v.mid[q] = word((uint32_t)q < y.nmid ? sb_addr(y.mid_s + q, 0) : dummy);
+  }
 
-  auto process = [&](size_t p, const Plan& y, Vals& v) {
+  __device__ __forceinline__ void process(size_t p, const Plan& y, Vals& v) const {
     if (y.len == 0) {  // crc of the empty string is 0; update mode leaves the register alone
       if constexpr (!UPD) g.out[p] = 0u;
       return;
@@ -268,7 +277,7 @@ __global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchArgs g) {
         for (uint32_t i = 0; i < y.nmid; i += 8) {
           if (i > 0) {
 #pragma unroll
-            for (int q = 0; q < 8; q++) v.mid[q] = gload4(sb_addr(y.mid_s + (i + q < y.nmid ? i + q : i), 0));
+            for (int q = 0; q < 8; q++) v.mid[q] = word(sb_addr(y.mid_s + (i + q < y.nmid ? i + q : i), 0));
           }
 #pragma unroll
           for (int q = 0; q < 8; q++)
@@ -301,34 +310,81 @@ __global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchArgs g) {
       acc = unshift(acc, 128 - y.te, lds);  // drop the zero bytes after the payload end
     }
     g.out[p] = UPD ? acc : ~acc;
-  };
+  }
+};
 
-  // contiguous payload ranges per block (coalesced descriptor loads), the same count for every block;
-  // the first payload's loads are in flight while the LDS image is staged
+__device__ __forceinline__ LaneCtx lane_ctx() {
+  LaneCtx k;
+  k.L0 = (threadIdx.x & 31) << 3;
+  k.L1 = k.L0 | (1u << 16);
+  k.slot4 = (threadIdx.x & 31) << 2;
+  return k;
+}
+
+// Second launch of the two-launch path: contiguous payload ranges per block (coalesced descriptor loads),
+// the same count for every block; the first payload's loads are in flight while the LDS image is staged.
+template <bool UPD, int BLK = kStitchBlock, int PROBE = 0>
+__global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchGeo g, const uint4* __restrict__ img_slice,
+                                                                 const uint4* __restrict__ img_stitch) {
+  __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsStitchImageBytes / 16];
+  const Stitcher<UPD, PROBE> st{g, reinterpret_cast<const uint32_t*>(lds4), lane_ctx()};
   const size_t per = (g.n + gridDim.x - 1) / gridDim.x;
   const size_t p_end = std::min(g.n, (size_t)(blockIdx.x + 1) * per);
   const size_t p_first = (size_t)blockIdx.x * per + threadIdx.x;
   Plan y{};
   Vals v{};
-  if (p_first < p_end) plan_and_load(p_first, y, v);
-  load_image<kLdsStitchImageBytes, BLK, kLdsCommonBytes>(lds4, g.img_slice, nullptr, g.img_stitch);
+  if (p_first < p_end) {
+    st.plan_a(p_first, y, v);
+    st.plan_b(p_first, y, v);
+  }
+  load_image<kLdsStitchImageBytes, BLK, kLdsCommonBytes>(lds4, img_slice, nullptr, img_stitch);
   __syncthreads();
   for (size_t p = p_first; p < p_end; p += BLK) {
-    if (p != p_first) plan_and_load(p, y, v);
-    process(p, y, v);
+    if (p != p_first) {
+      st.plan_a(p, y, v);
+      st.plan_b(p, y, v);
+    }
+    st.process(p, y, v);
   }
 }
 
+// First launch: the line pass.
+template <int PROBE = 0>
+__global__ __launch_bounds__(kBlock) void crc32_arena_lines_kernel(const uint8_t* __restrict__ base, LineOut ar,
+                                                                   const uint4* __restrict__ img_slice,
+                                                                   const uint4* __restrict__ img_group8,
+                                                                   const uint4* __restrict__ img_sb) {
+  __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsArenaImageBytes / 16];
+  arena_line_pass<PROBE>(base, ar, blockIdx.x, gridDim.x, lds4, img_slice, img_group8, img_sb);
+}
+
 }  // namespace
+
+LineOut line_out(const ArenaLaunch& a, const ArenaGeom& geo) {
+  LineOut ar;
+  ar.S = a.scratch;
+  ar.SB = a.scratch + geo.sb_off;
+  ar.S_edge = a.scratch + geo.edge_off;
+  ar.SB_edge = ar.S_edge + 128;
+  ar.W = geo.W;
+  ar.byte_lo = a.byte_lo;
+  ar.byte_hi = a.byte_hi;
+  ar.line_lo = a.line_lo;
+  ar.line_hi = a.line_hi;
+  ar.sb0 = a.sb0;
+  ar.nsb = a.nsb;
+  ar.fs0 = a.fs0;
+  ar.fs1 = a.fs1;
+  ar.zero_line = (uint64_t)(uintptr_t)a.zero_line;
+  return ar;
+}
 
 size_t stitch_blocks(const ArenaLaunch& a) {
   return std::max<size_t>(1, std::min<size_t>(a.max_blocks, (a.n + kStitchBlock - 1) / kStitchBlock));
 }
 
-template <int PROBE>
-hipError_t launch_stitch_p(const ArenaLaunch& a, hipStream_t stream) {
-  const ArenaGeom geo = arena_geom(a);
-  StitchArgs s;
+StitchGeo stitch_geo(const ArenaLaunch& a, const ArenaGeom& geo) {
+  StitchGeo s;
   s.base = static_cast<const uint8_t*>(a.base);
   s.byte_lo = a.byte_lo;
   s.byte_hi = a.byte_hi;
@@ -337,30 +393,50 @@ hipError_t launch_stitch_p(const ArenaLaunch& a, hipStream_t stream) {
   s.sb0 = a.sb0;
   s.fs0 = a.fs0;
   s.fs1 = a.fs1;
-  s.lg = geo.lg;
+  s.W = geo.W;
+  s.L = (uint32_t)geo.blocks;
   s.S = a.scratch;
   s.SB = a.scratch ? a.scratch + geo.sb_off : nullptr;
   s.S_edge = a.scratch ? a.scratch + geo.edge_off : nullptr;
+  s.SB_edge = a.scratch ? a.scratch + geo.edge_off + 128 : nullptr;
   s.off = a.off;
   s.len = a.len;
   s.n = a.n;
-  s.img_slice = static_cast<const uint4*>(a.img_slice);
-  s.img_stitch = static_cast<const uint4*>(a.img_stitch);
   s.zero_line = (uint64_t)(uintptr_t)a.zero_line;
   s.out = a.out;
+  return s;
+}
+
+template <int PROBE>
+hipError_t launch_stitch_p(const ArenaLaunch& a, hipStream_t stream) {
+  const StitchGeo s = stitch_geo(a, arena_geom(a));
   const size_t blocks = stitch_blocks(a);
+  const uint4* img_slice = static_cast<const uint4*>(a.img_slice);
+  const uint4* img_stitch = static_cast<const uint4*>(a.img_stitch);
   if (a.update)
     hipLaunchKernelGGL((crc32_arena_stitch_kernel<true, kStitchBlock, PROBE>), dim3((unsigned)blocks),
-                       dim3(kStitchBlock), 0, stream, s);
+                       dim3(kStitchBlock), 0, stream, s, img_slice, img_stitch);
   else
     hipLaunchKernelGGL((crc32_arena_stitch_kernel<false, kStitchBlock, PROBE>), dim3((unsigned)blocks),
-                       dim3(kStitchBlock), 0, stream, s);
+                       dim3(kStitchBlock), 0, stream, s, img_slice, img_stitch);
   return hipGetLastError();
 }
 
+template <int PROBE>
+hipError_t launch_arena_lines_p(const ArenaLaunch& a, hipStream_t stream) {
+  static_assert(kBlock / 8 == 64 && kSTasks == 8, "arena_geom / arena_s_word assume 64 groups per block, 8-task bursts");
+  const ArenaGeom geo = arena_geom(a);
+  hipLaunchKernelGGL((crc32_arena_lines_kernel<PROBE>), dim3((unsigned)geo.blocks), dim3(kBlock), 0, stream,
+                     reinterpret_cast<const uint8_t*>((uintptr_t)(a.fs0 * 8192)), line_out(a, geo), static_cast<const uint4*>(a.img_slice), static_cast<const uint4*>(a.img_group8),
+                     static_cast<const uint4*>(a.img_sb));
+  return hipGetLastError();
+}
+
+hipError_t launch_arena_lines(const ArenaLaunch& a, hipStream_t stream) { return launch_arena_lines_p<0>(a, stream); }
+
 hipError_t launch_arena(const ArenaLaunch& a, hipStream_t stream) {
   if (a.nsb) {
-    const hipError_t e = launch_arena_lines(a, stream);  // crc32_kernels.hip
+    const hipError_t e = launch_arena_lines(a, stream);
     if (e != hipSuccess) return e;
   }
   return launch_stitch_p<0>(a, stream);

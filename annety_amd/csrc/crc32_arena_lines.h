@@ -1,0 +1,152 @@
+// The arena line pass (crc32_arena_lines_kernel in crc32_arena.hip): the config-1 kernel's
+// loop over full 8 KiB superblocks (a wave = 64 consecutive 128-byte lines per task, A/B register double
+// buffer, unconditional next-task loads), storing per line the block-suffix CRC S and per block the
+// superblock-suffix SB (layout: crc32_kernels.h). Included by crc32_arena.hip only.
+#pragma once
+
+#include "crc32_device.h"
+#include "crc32_kernels.h"
+
+namespace annety_crc {
+namespace {
+
+struct LineOut {
+  uint32_t *S, *SB, *S_edge, *SB_edge;
+  uint64_t W;  // line-pass waves = 8 * workgroups
+  uint64_t byte_lo, byte_hi, line_lo, line_hi, sb0, nsb, fs0, fs1;
+  uint64_t zero_line;
+};
+
+//   PROBE (microbench only; product = 0): bit 0 drops the S stores, bit 1 the superblock scan - wrong
+//   outputs, used to measure what those stages cost.
+// `base` = the first full superblock (fs0 * 8192), passed as its own kernel argument: loads through a
+// __restrict__ kernel-argument pointer compile to the config-1 kernel's schedule; the same loads through
+// integer-built address-space-1 pointers ran this pass 30 % slower (microbench/arena_mb.hip).
+template <int PROBE = 0>
+__device__ __forceinline__ void arena_line_pass(const uint8_t* __restrict__ base, const LineOut& ar, uint32_t bid,
+                                                uint32_t nbid, uint4* lds4,
+                                                const uint4* __restrict__ img_slice,
+                                                const uint4* __restrict__ img_group8,
+                                                const uint4* __restrict__ img_sb) {
+  constexpr int BLK = kBlock, VWG = kVwg;
+  const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
+  const uint32_t j = threadIdx.x & 7;
+  const size_t gid = (((size_t)bid + (size_t)nbid * (threadIdx.x / VWG)) * VWG + threadIdx.x % VWG) / 8;
+  const size_t ngroups = (size_t)nbid * (BLK / 8);
+  const size_t n = (size_t)(ar.fs1 - ar.fs0) * 8;  // full 1 KiB blocks = lane-group tasks
+  const int ntasks = gid < n ? (int)((n - 1 - gid) / ngroups + 1) : 0;
+  const uint64_t pstep = ngroups * 1024;
+
+  LaneCtx k;
+  k.L0 = (threadIdx.x & 31) << 3;
+  k.L1 = k.L0 | (1u << 16);
+  k.slot4 = (threadIdx.x & 31) << 2;
+
+  const uint8_t* lp = base + gid * 1024 + (size_t)j * kChunkBytes;
+  uint4 A[8], B[8];
+  if (ntasks > 0) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) A[i] = reinterpret_cast<const uint4*>(lp)[i];
+  }
+  load_image<kLdsArenaImageBytes, BLK>(lds4, img_slice, img_group8, img_sb);
+  __syncthreads();
+
+  const uint32_t lane = threadIdx.x & 63;
+  // S of 8 consecutive tasks leaves in two 16-byte stores per lane, each 1 KiB contiguous per wave:
+  // interleaved with the read stream, a dword per lane per task cost 30 us of a 211 us pass, 16-byte
+  // quads of 4 tasks 20 (microbench/arena_mb.hip).
+  uint32_t q[kSTasks];
+#pragma unroll
+  for (uint32_t i = 0; i < kSTasks; i++) q[i] = 0;
+  // r = raw CRC of this lane's line; returns S for it and (lanes j == 0) SB for its block
+  auto arena_scan = [&](uint32_t r, uint32_t& sbv) {
+    uint32_t x = nibble_map_lane(r, lds, k.slot4);  // shift_{(7-j)*128}(r): the line seen from the block end
+    // suffix scan over the 8 lanes of the group (DPP row_shl:d = the value of lane + d in its row of 16)
+    uint32_t y;
+    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x101, 0xF, 0xF, false);
+    x ^= j + 1 < 8 ? y : 0u;
+    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x102, 0xF, 0xF, false);
+    x ^= j + 2 < 8 ? y : 0u;
+    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x104, 0xF, 0xF, false);
+    x ^= j + 4 < 8 ? y : 0u;  // S: lines j..7
+    sbv = 0;
+    if constexpr ((PROBE & 2) == 0) {
+      // the 8 groups of a wave are one superblock, in order (g = lane / 8): block g seen from the
+      // superblock end on lane 8g, then the suffix scan of those 8 values in scalar registers
+      const uint32_t g = lane >> 3;
+      uint32_t u = 0;
+      if (j == 0) u = sb_join(x, lds, g);
+      uint32_t t[8];
+      t[7] = (uint32_t)__builtin_amdgcn_readlane((int)u, 56);
+#pragma unroll
+      for (int h = 6; h >= 0; h--) t[h] = t[h + 1] ^ (uint32_t)__builtin_amdgcn_readlane((int)u, 8 * h);
+      sbv = t[0];
+#pragma unroll
+      for (uint32_t h = 1; h < 8; h++) sbv = g == h ? t[h] : sbv;  // SB: blocks g..7
+    }
+    return x;
+  };
+  // partial superblocks at the arena ends (wave-uniform, two waves of the grid)
+  const uint64_t gw = (uint64_t)bid * (BLK / 64) + (threadIdx.x >> 6);
+  if (gw < 2) {
+    const uint64_t sb = gw == 0 ? ar.sb0 : ar.sb0 + ar.nsb - 1;
+    if ((sb < ar.fs0 || sb >= ar.fs1) && (gw == 0 || sb != ar.sb0)) {
+      const uint64_t line = sb * 64 + lane;
+      const bool in = line >= ar.line_lo && line <= ar.line_hi;
+      const uint64_t src = in ? line << 7 : ar.zero_line;
+      uint4 v[8];
+#pragma unroll
+      for (int i = 0; i < 8; i++) v[i] = gload16(src + 16 * i);
+      const int32_t lo8 = line == ar.line_lo ? (int32_t)(ar.byte_lo & 127) * 8 : 0;
+      const int32_t hi8 = line == ar.line_hi ? (int32_t)(((ar.byte_hi - 1) & 127) + 1) * 8 : 1024;
+      mask_line(v, lo8, hi8);
+      uint32_t sbv;
+      const uint32_t x = arena_scan(absorb_line(0u, v, k, lds), sbv);
+      if constexpr ((PROBE & 1) == 0) ar.S_edge[gw * 64 + lane] = x;
+      if (j == 0) ar.SB_edge[gw * 8 + (lane >> 3)] = sbv;
+    }
+  }
+
+  auto finish = [&](uint32_t s, int t) {
+    uint32_t sbv;
+    const uint32_t x = arena_scan(s, sbv);
+    const uint32_t slot = (uint32_t)t & (kSTasks - 1);
+#pragma unroll
+    for (uint32_t i = 0; i < kSTasks; i++) q[i] = slot == i ? x : q[i];
+    if constexpr ((PROBE & 2) == 0) {
+      if (j == 0) ar.SB[(((uint64_t)t * ngroups + gid) / 8) * 8 + (lane >> 3)] = sbv;
+    }
+    if (slot == kSTasks - 1 || t + 1 == ntasks) {
+      const uint64_t t0 = (uint64_t)t & ~7ull;
+      if constexpr ((PROBE & 1) == 0) {
+        const v4u32 lo = {q[0], q[1], q[2], q[3]}, hi = {q[4], q[5], q[6], q[7]};
+        v4u32* dst = reinterpret_cast<v4u32*>(ar.S + arena_s_word(t0, gid, j, ar.W));
+        __builtin_nontemporal_store(lo, dst);
+        __builtin_nontemporal_store(hi, dst + 64);  // + 1 KiB
+      }
+    }
+  };
+  // Loads are unconditional (past the last task a group re-reads its current line, an L2 hit): with the
+  // next task's loads behind a branch the waitcnt pass merges the two paths and waits vmcnt(0) before
+  // every fold, which serialises the A/B double buffer.
+  for (int t = 0; t < ntasks; t += 2) {
+    {
+      const uint4* s = reinterpret_cast<const uint4*>(t + 1 < ntasks ? lp + pstep : lp);
+#pragma unroll
+      for (int i = 0; i < 8; i++) B[i] = s[i];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    finish(absorb_line(0u, A, k, lds), t);
+    {
+      const uint4* s = reinterpret_cast<const uint4*>(t + 2 < ntasks ? lp + 2 * pstep : lp);
+#pragma unroll
+      for (int i = 0; i < 8; i++) A[i] = s[i];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + 1 < ntasks) finish(absorb_line(0u, B, k, lds), t + 1);
+    lp += 2 * pstep;
+  }
+}
+
+}  // namespace
+}  // namespace annety_crc

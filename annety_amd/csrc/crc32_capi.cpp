@@ -503,6 +503,7 @@ int run_arena(DeviceCtx& c, const void* d_base, size_t arena_bytes, const uint64
   a.n = n;
   a.out = d_out;
   a.update = update;
+  if (n == 0) return ANNETY_CRC_OK;
   if (!a.nsb) {
     const hipError_t e = launch_arena(a, stream);
     return e == hipSuccess ? ANNETY_CRC_OK : hip_fail(e);

@@ -175,19 +175,21 @@ __device__ __forceinline__ uint32_t group_xor_reduce(uint32_t x) {
 // Parts: slicing tables (img_slice), the per-G join/round tables (img_group) and, for the
 // variable-length kernel, the inverse-shift tables (img_extra).
 // kBaseBytes: end of the group part (the extra part follows it; = kLdsCommonBytes for images with
-// no group part).
-template <uint32_t kBytes = kLdsImageBytes, int BLK = kBlock, uint32_t kBaseBytes = kLdsImageBytes>
+// no group part). kStartBytes: stage only [kStartBytes, kBytes) (the rest is already in place).
+template <uint32_t kBytes = kLdsImageBytes, int BLK = kBlock, uint32_t kBaseBytes = kLdsImageBytes,
+          uint32_t kStartBytes = 0>
 __device__ __forceinline__ void load_image(uint4* lds4, const uint4* __restrict__ img_common,
                                            const uint4* __restrict__ img_group,
                                            const uint4* __restrict__ img_extra = nullptr) {
   constexpr int kCommon = kLdsCommonBytes / 16;
   constexpr int kBase = kBaseBytes / 16;
   constexpr int kTotal = kBytes / 16;
+  constexpr int kStart = kStartBytes / 16;
   constexpr int kChunks = (kTotal + 63) / 64;  // 1 KiB pieces (the last one may be partial)
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  for (int c = wave; c < kChunks; c += BLK / 64) {
+  for (int c = kStart / 64 + wave; c < kChunks; c += BLK / 64) {
     const int i = c * 64 + lane;
-    if (i < kTotal) {
+    if (i >= kStart && i < kTotal) {
       const uint4* src = i < kCommon ? img_common + i : (i < kBase ? img_group + (i - kCommon) : img_extra + (i - kBase));
       __builtin_amdgcn_global_load_lds(src, lds4 + c * 64, 16, 0, 0);
     }

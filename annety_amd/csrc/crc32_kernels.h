@@ -88,43 +88,50 @@ struct ArenaLaunch {
   bool update;
 };
 
-// S of the full superblocks: kSTasks = 8 consecutive tasks of a wave leave together, as two 16-byte
-// stores per lane that each cover 1 KiB contiguously. Task t of lane-group `group`, line a, lives at word
-//   ((((t / 8) << (lg - 3)) + group / 8) * 2 + (t % 8) / 4) * 256 + ((group % 8) * 8 + a) * 4 + t % 4.
+// Line-pass layout. L line-pass workgroups of 512 lanes = W = 8L waves = 64L lane groups;
+// wave w's task t is full superblock fs0 + t*W + w (lane group g = 8w + block). Per line of a full
+// superblock the block-suffix CRC S leaves in bursts of 8 tasks, two 16-byte stores per lane that each
+// cover 1 KiB contiguously: task t of group g, line a at word
+//   ((((t / 8) * W + g / 8) * 2 + (t / 4) % 2) * 256 + ((g % 8) * 8 + a) * 4 + t % 4.
+// SB (superblock suffix per block) of full superblock fs0 + i, block g at word i * 8 + g: a 128-byte line
+// holds 4 superblocks of one task (W is a multiple of 4), so no line mixes two tasks' stores. The (at
+// most two) partial superblocks keep S in S_edge[2][64] and SB in SB_edge[2][8].
 constexpr uint32_t kSTasks = 8;
-inline __host__ __device__ uint64_t arena_s_word(uint64_t t, uint64_t group, uint32_t a, uint32_t lg) {
-  return (((((t >> 3) << (lg - 3)) + (group >> 3)) * 2 + ((t >> 2) & 1)) << 8) + (((group & 7) * 8 + a) << 2) +
-         (t & 3);
+inline __host__ __device__ uint64_t arena_s_word(uint64_t t, uint64_t group, uint32_t a, uint64_t W) {
+  return ((((t >> 3) * W + (group >> 3)) * 2 + ((t >> 2) & 1)) << 8) + (((group & 7) * 8 + a) << 2) + (t & 3);
 }
 
-// Line-pass geometry: the grid (a power of two of 512-lane blocks, so lane-group and task of a block
-// are a mask and a shift), and the scratch layout [S bursts | SB nsb x 8 | S_edge 2 x 64] in words.
+// Geometry of one arena call: the line pass on `blocks` workgroups, and the scratch layout
+// [S | SB | S_edge 128 | SB_edge 16].
 struct ArenaGeom {
-  size_t blocks;      // line-pass workgroups
-  uint32_t lg;        // log2(lane-groups) = log2(blocks * 64)
-  uint64_t sb_off;    // word offset of SB (= words of the S bursts)
-  uint64_t edge_off;  // word offset of S_edge
-  uint64_t words;     // total
+  size_t blocks;         // line-pass workgroups L
+  uint64_t W;            // line-pass waves = 8L
+  uint64_t ntasks;       // tasks of the busiest wave
+  uint64_t nbursts;      // ceil(ntasks / 8)
+  uint64_t sb_off, edge_off, words;
 };
-inline ArenaGeom arena_geom(const ArenaLaunch& a) {
+inline ArenaGeom arena_geom(const ArenaLaunch& a, size_t line_blocks) {  // line_blocks >= 1
   ArenaGeom g{};
-  const uint64_t nblk = (a.fs1 - a.fs0) * 8;  // full 1 KiB blocks, one per lane-group task
-  uint64_t want = (nblk + 63) / 64;
-  if (want > a.max_blocks) want = a.max_blocks;
-  g.blocks = 1;
-  while (g.blocks * 2 <= want) g.blocks *= 2;
-  g.lg = 6;
-  while ((1ull << (g.lg - 6)) < g.blocks) g.lg++;
-  const uint64_t ngroups = (uint64_t)1 << g.lg;
-  const uint64_t bursts = ((nblk + ngroups - 1) / ngroups + kSTasks - 1) / kSTasks;
-  g.sb_off = bursts * ngroups * 8 * kSTasks;
-  g.edge_off = g.sb_off + a.nsb * 8;
-  g.words = g.edge_off + 128;
+  const uint64_t nsbf = a.fs1 - a.fs0;  // full superblocks
+  g.blocks = line_blocks ? line_blocks : 1;
+  g.W = 8 * (uint64_t)g.blocks;
+  g.ntasks = (nsbf + g.W - 1) / g.W;
+  g.nbursts = (g.ntasks + kSTasks - 1) / kSTasks;
+  g.sb_off = g.nbursts * g.W * 512;
+  g.edge_off = g.sb_off + nsbf * 8;
+  g.words = g.edge_off + 144;
   return g;
+}
+// The line pass on min(max_blocks, what the arena fills) workgroups.
+inline ArenaGeom arena_geom(const ArenaLaunch& a) {
+  const uint64_t nsbf = a.fs1 - a.fs0;
+  uint64_t want = nsbf / 8 + 1;  // a wave per superblock per task, 8 waves per workgroup
+  if (want > a.max_blocks) want = a.max_blocks;
+  return arena_geom(a, (size_t)want);
 }
 
 hipError_t launch_arena(const ArenaLaunch& a, hipStream_t stream);
-// the line pass alone (crc32_kernels.hip: the config-1 kernel in arena mode)
+// the line pass alone (crc32_arena.hip, crc32_arena_lines.h)
 hipError_t launch_arena_lines(const ArenaLaunch& a, hipStream_t stream);
 
 // LengthHeaderCodec frames (crc32_frames.hip)

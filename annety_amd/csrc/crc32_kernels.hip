@@ -136,39 +136,16 @@ __global__ __launch_bounds__(kBlock) void crc32_fixed_kernel(const uint8_t* __re
   }
 }
 
-// Arena-mode arguments (crc32_arena.hip). The main loop streams the arena's FULL
-// superblocks [fs0, fs1) as 1 KiB blocks (base = superblock fs0, stride 1 KiB, G = 8); the partial
-// superblocks at the two ends, if any, are done first by global waves 0 and 1, whose bytes outside the
-// arena [byte_lo, byte_hi) read as zeros (the zero line, or a byte mask on the two boundary lines).
-// Outputs, per line j of a 1 KiB block b: the suffix CRC S = raw(lines j..7 of b); per block g of a
-// superblock: SB = raw(blocks g..7 of the superblock). S of the full superblocks is stored in task-major
-// bursts (8 consecutive tasks together: arena_s_word in crc32_kernels.h), S of the partial ones in
-// S_edge[2][64]; SB as [superblock - sb0][g], one 32-byte store per superblock (in bursts from the 8
-// leader lanes the same bytes cost 11 us more: microbench/arena_mb.hip).
-struct ArenaOut {
-  uint32_t *S, *S_edge, *SB;
-  uint32_t lg;  // log2(lane-groups of the grid)
-  uint64_t byte_lo, byte_hi, line_lo, line_hi, sb0, nsb, fs0, fs1;
-  uint64_t zero_line;
-};
-
 // Single-round fast path (payload = exactly G lines, 16-byte aligned; BASELINE config 1 is G = 8):
 // each step is one whole payload per lane-group, so there is no round state, and the per-lane line
-// pointer advances by a constant per task. Loads run one task ahead (A/B double buffer).
-//   ARENA (G = 8): the arena line pass instead of digests (ArenaOut above): per line the raw CRC
-//   (register 0, no init) mapped to its block end, the block's suffix scan S, and across the 8 groups of
-//   a wave (one superblock) the suffix scan SB.
-//   PROBE (microbench only; product = 0, ARENA only): bit 0 drops the S store, bit 1 the superblock
-//   scan - wrong outputs, used to measure what those stages cost.
-template <int G, int BLK = kBlock, int VWG = kVwg, bool ARENA = false, int PROBE = 0>
+// pointer advances by a constant per task. Loads run one task ahead (A/B double buffer). The arena line
+// pass (crc32_arena_lines.h) is this loop with suffix-CRC outputs instead of digests.
+template <int G, int BLK = kBlock, int VWG = kVwg>
 __global__ __launch_bounds__(BLK) void crc32_oneround_kernel(const uint8_t* __restrict__ base, size_t n,
                                                                 size_t stride, const uint4* __restrict__ img_slice,
                                                                 const uint4* __restrict__ img_group,
-                                                                uint32_t* __restrict__ out,
-                                                                const uint4* __restrict__ img_sb = nullptr,
-                                                                ArenaOut ar = {}) {
-  constexpr uint32_t kImage = ARENA ? kLdsArenaImageBytes : kLdsImageBytes;
-  __shared__ __attribute__((aligned(16))) uint4 lds4[kImage / 16];
+                                                                uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsImageBytes / 16];
   const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
 
   const uint32_t j = threadIdx.x & (G - 1);
@@ -181,7 +158,7 @@ __global__ __launch_bounds__(BLK) void crc32_oneround_kernel(const uint8_t* __re
   k.L0 = (threadIdx.x & 31) << 3;
   k.L1 = k.L0 | (1u << 16);
   k.slot4 = (threadIdx.x & 31) << 2;
-  const uint32_t sinit = (!ARENA && j == 0) ? kInit : 0u;  // init == complement of the payload's first word
+  const uint32_t sinit = j == 0 ? kInit : 0u;  // init == complement of the payload's first word
 
   const uint8_t* lp = base + gid * stride + (size_t)j * kChunkBytes;
   uint32_t* op = out + gid;
@@ -190,93 +167,14 @@ __global__ __launch_bounds__(BLK) void crc32_oneround_kernel(const uint8_t* __re
 #pragma unroll
     for (int i = 0; i < 8; i++) A[i] = reinterpret_cast<const uint4*>(lp)[i];
   }
-  load_image<kImage, BLK>(lds4, img_slice, img_group, img_sb);
+  load_image<kLdsImageBytes, BLK>(lds4, img_slice, img_group);
   __syncthreads();
 
-  const uint32_t lane = threadIdx.x & 63;
-  // S of 8 consecutive tasks leaves in two 16-byte nontemporal stores per lane, each 1 KiB contiguous
-  // per wave: interleaved with the read stream, a dword per lane per task cost 30 us of a 211 us pass,
-  // 16-byte quads of 4 tasks 20 (microbench/arena_mb.hip).
-  uint32_t q[kSTasks];
-#pragma unroll
-  for (uint32_t i = 0; i < kSTasks; i++) q[i] = 0;
-  // r = raw CRC of this lane's line, b = its block (relative to sb0); returns S for this lane's line
-  // r = raw CRC of this lane's line; returns S for it and (lanes j == 0) SB for its block
-  auto arena_scan = [&](uint32_t r, uint32_t& sbv) {
-    uint32_t x = nibble_map_lane(r, lds, k.slot4);  // shift_{(7-j)*128}(r): the line seen from the block end
-    // suffix scan over the 8 lanes of the group (DPP row_shl:d = the value of lane + d in its row of 16)
-    uint32_t y;
-    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x101, 0xF, 0xF, false);
-    x ^= j + 1 < 8 ? y : 0u;
-    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x102, 0xF, 0xF, false);
-    x ^= j + 2 < 8 ? y : 0u;
-    y = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x104, 0xF, 0xF, false);
-    x ^= j + 4 < 8 ? y : 0u;  // S: lines j..7
-    sbv = 0;
-    if constexpr ((PROBE & 2) == 0) {
-      // the 8 groups of a wave are one superblock, in order (g = lane / 8): block g seen from the
-      // superblock end on lane 8g, then the suffix scan of those 8 values in scalar registers
-      const uint32_t g = lane >> 3;
-      uint32_t u = 0;
-      if (j == 0) u = sb_join(x, lds, g);
-      uint32_t t[8];
-      t[7] = (uint32_t)__builtin_amdgcn_readlane((int)u, 56);
-#pragma unroll
-      for (int h = 6; h >= 0; h--) t[h] = t[h + 1] ^ (uint32_t)__builtin_amdgcn_readlane((int)u, 8 * h);
-      sbv = t[0];
-#pragma unroll
-      for (uint32_t h = 1; h < 8; h++) sbv = g == h ? t[h] : sbv;  // SB: blocks g..7
-    }
-    return x;
-  };
-  if constexpr (ARENA) {
-    // partial superblocks at the arena ends (wave-uniform, two waves of the grid)
-    const uint64_t gw = (uint64_t)blockIdx.x * (BLK / 64) + (threadIdx.x >> 6);
-    if (gw < 2) {
-      const uint64_t sb = gw == 0 ? ar.sb0 : ar.sb0 + ar.nsb - 1;
-      if ((sb < ar.fs0 || sb >= ar.fs1) && (gw == 0 || sb != ar.sb0)) {
-        const uint64_t line = sb * 64 + lane;
-        const bool in = line >= ar.line_lo && line <= ar.line_hi;
-        const uint64_t src = in ? line << 7 : ar.zero_line;
-        uint4 v[8];
-#pragma unroll
-        for (int i = 0; i < 8; i++) v[i] = gload16(src + 16 * i);
-        const int32_t lo8 = line == ar.line_lo ? (int32_t)(ar.byte_lo & 127) * 8 : 0;
-        const int32_t hi8 = line == ar.line_hi ? (int32_t)(((ar.byte_hi - 1) & 127) + 1) * 8 : 1024;
-        mask_line(v, lo8, hi8);
-        uint32_t sbv;
-        const uint32_t x = arena_scan(absorb_line(0u, v, k, lds), sbv);
-        if constexpr ((PROBE & 1) == 0) ar.S_edge[gw * 64 + lane] = x;
-        if (j == 0) ar.SB[(sb - ar.sb0) * 8 + (lane >> 3)] = sbv;
-      }
-    }
-  }
-
-  auto finish = [&](uint32_t s, int t) {
-    if constexpr (ARENA) {
-      uint32_t sbv;
-      const uint32_t x = arena_scan(s, sbv);
-      const uint32_t slot = (uint32_t)t & (kSTasks - 1);
-#pragma unroll
-      for (uint32_t i = 0; i < kSTasks; i++) q[i] = slot == i ? x : q[i];
-      if constexpr ((PROBE & 2) == 0) {
-        if (j == 0) ar.SB[(ar.fs0 - ar.sb0 + (((uint64_t)t << ar.lg) + gid) / 8) * 8 + (lane >> 3)] = sbv;
-      }
-      if (slot == kSTasks - 1 || t + 1 == ntasks) {
-        const uint64_t t0 = (uint64_t)t & ~7ull;
-        if constexpr ((PROBE & 1) == 0) {
-          v4u32* dst = reinterpret_cast<v4u32*>(ar.S + arena_s_word(t0, gid, j, ar.lg));
-          const v4u32 lo = {q[0], q[1], q[2], q[3]}, hi = {q[4], q[5], q[6], q[7]};
-          __builtin_nontemporal_store(lo, dst);
-          __builtin_nontemporal_store(hi, dst + 64);  // + 1 KiB
-        }
-      }
-    } else {
-      uint32_t u = s;
-      if constexpr (G > 1) u = group_xor_reduce<G>(nibble_map_lane(s, lds, k.slot4));
-      if (j == G - 1) *op = ~u;
-      op += ngroups;
-    }
+  auto finish = [&](uint32_t s) {
+    uint32_t t = s;
+    if constexpr (G > 1) t = group_xor_reduce<G>(nibble_map_lane(s, lds, k.slot4));
+    if (j == G - 1) *op = ~t;
+    op += ngroups;
   };
   // Loads are unconditional (past the last task a group re-reads its current line, an L2 hit): with the
   // next task's loads behind a branch the waitcnt pass merges the two paths and waits vmcnt(0) before
@@ -288,14 +186,14 @@ __global__ __launch_bounds__(BLK) void crc32_oneround_kernel(const uint8_t* __re
       for (int i = 0; i < 8; i++) B[i] = s[i];
     }
     __builtin_amdgcn_sched_barrier(0);
-    finish(absorb_line(sinit, A, k, lds), t);
+    finish(absorb_line(sinit, A, k, lds));
     {
       const uint4* s = reinterpret_cast<const uint4*>(t + 2 < ntasks ? lp + 2 * pstep : lp);
 #pragma unroll
       for (int i = 0; i < 8; i++) A[i] = s[i];
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (t + 1 < ntasks) finish(absorb_line(sinit, B, k, lds), t + 1);
+    if (t + 1 < ntasks) finish(absorb_line(sinit, B, k, lds));
     lp += 2 * pstep;
   }
 }
@@ -757,35 +655,7 @@ hipError_t launch_full(const FixedLaunch& a, hipStream_t stream) {
   }
 }
 
-template <int PROBE>
-hipError_t launch_arena_lines_p(const ArenaLaunch& a, hipStream_t stream) {
-  const ArenaGeom geo = arena_geom(a);
-  ArenaOut ar;
-  ar.S = a.scratch;
-  ar.SB = a.scratch + geo.sb_off;
-  ar.S_edge = a.scratch + geo.edge_off;
-  ar.lg = geo.lg;
-  ar.byte_lo = a.byte_lo;
-  ar.byte_hi = a.byte_hi;
-  ar.line_lo = a.line_lo;
-  ar.line_hi = a.line_hi;
-  ar.sb0 = a.sb0;
-  ar.nsb = a.nsb;
-  ar.fs0 = a.fs0;
-  ar.fs1 = a.fs1;
-  ar.zero_line = (uint64_t)(uintptr_t)a.zero_line;
-  static_assert(kBlock / 8 == 64 && kSTasks == 8, "arena_geom / arena_s_word assume 64 groups per block, 8-task bursts");
-  const size_t nblk = (size_t)(a.fs1 - a.fs0) * 8;  // full 1 KiB blocks
-  hipLaunchKernelGGL((crc32_oneround_kernel<8, kBlock, kVwg, true, PROBE>), dim3((unsigned)geo.blocks), dim3(kBlock),
-                     0, stream, reinterpret_cast<const uint8_t*>((uintptr_t)(a.fs0 * 8192)), nblk, (size_t)1024,
-                     static_cast<const uint4*>(a.img_slice), static_cast<const uint4*>(a.img_group8), nullptr,
-                     static_cast<const uint4*>(a.img_sb), ar);
-  return hipGetLastError();
-}
-
 }  // namespace
-
-hipError_t launch_arena_lines(const ArenaLaunch& a, hipStream_t stream) { return launch_arena_lines_p<0>(a, stream); }
 
 hipError_t launch_fixed(const FixedLaunch& a, hipStream_t stream) {
   if (!a.raw && a.full && a.rounds == 1) return launch_one(a, stream);
