@@ -151,8 +151,8 @@ class Workload:
             self.payload_bytes = total
             self.algo_bytes = total + 4 * self.n + 12 * self.n  # + offset/length metadata reads
             self.arena = args.var_path == "arena"
-            self.kernel = ("crc32_oneround_kernel<8, arena> + crc32_arena_stitch_kernel, one step "
-                           "(annety_amd/csrc/crc32_kernels.hip, crc32_arena.hip)" if self.arena else
+            self.kernel = ("crc32_arena_lines_kernel + crc32_arena_stitch_kernel, one step "
+                           "(annety_amd/csrc/crc32_arena.hip, crc32_arena_lines.h)" if self.arena else
                            "crc32_bucket_hist/scan/scatter + crc32_var_kernel<32/8/2>, one step "
                            "(annety_amd/csrc/crc32_kernels.hip)")
             self.desc = (f"BASELINE config 3: {self.n} payloads, Zipf(1.1) lengths 64 B-64 KiB packed unaligned, "

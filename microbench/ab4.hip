@@ -2,6 +2,7 @@
 // bucket passes alone, each length class alone, and the classes without byte masks / unshift
 // (PROBE variants: wrong digests by design, timing only).
 #include "../annety_amd/csrc/crc32_kernels.hip"
+#include "../annety_amd/csrc/crc32_arena.hip"
 #include "../annety_amd/csrc/crc32_frames.hip"
 #include "../annety_amd/csrc/crc32_capi.cpp"
 #include <cmath>
