@@ -462,7 +462,7 @@ int run_var_sorted(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d
   int rc = ANNETY_CRC_OK;
   hipError_t e = launch_bucket(d_base, n, d_off, d_len, rows, ranges, desc, update ? nullptr : d_out, stream);
   if (e != hipSuccess) rc = hip_fail(e);
-  const uint32_t groups[3] = {32, 8, 2};
+  const uint32_t groups[3] = {32, 16, 4};  // lanes per payload of the long / middle / small class
   for (int k = 0; k < 3 && rc == ANNETY_CRC_OK; k++)
     rc = run_var(c, d_base, n, 0, 0, groups[k], desc, ranges + 2 * k, d_out, stream, update);
   e = hipFreeAsync(scratch, stream);

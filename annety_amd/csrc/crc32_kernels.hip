@@ -485,16 +485,17 @@ __global__ __launch_bounds__(kBuckets) void crc32_bucket_scan(uint32_t* __restri
     rows[(size_t)b * kBuckets + i] = run;
     run += c;
   }
-  // classes by line count (bucket = 1023 - lines): G=32 >= 128 lines, G=8 24..127, G=2 < 24.
-  // Chosen to keep virtual (idle) lines near 5 % on a Zipf(1.1) 64 B-64 KiB batch.
-  constexpr int b8 = kBuckets - 128, b2 = kBuckets - 24;  // first bucket of the G=8 / G=2 classes
+  // classes by line count (bucket = 1023 - lines): >= 128 lines, 24..127, < 24, run at G = 32 / 16 / 4
+  // (crc32_capi.cpp run_var_sorted; on the config-3 batch the middle and small classes ran 12 % and
+  // 15 % faster at G = 16 / 4 than at 8 / 2: profiles/r02/ab4_stages.log).
+  constexpr int b8 = kBuckets - 128, b2 = kBuckets - 24;  // first bucket of the middle / small classes
   if (i == 0) {
     ranges[0] = 0;
-    ranges[1] = sc[b8 - 1];        // G=32 class: buckets [0, b8)
+    ranges[1] = sc[b8 - 1];        // long class: buckets [0, b8)
     ranges[2] = sc[b8 - 1];
-    ranges[3] = sc[b2 - 1];        // G=8 class: buckets [b8, b2)
+    ranges[3] = sc[b2 - 1];        // middle class: buckets [b8, b2)
     ranges[4] = sc[b2 - 1];
-    ranges[5] = sc[kBuckets - 1];  // G=2 class: buckets [b2, kBuckets)
+    ranges[5] = sc[kBuckets - 1];  // small class: buckets [b2, kBuckets)
   }
 }
 
