@@ -76,6 +76,21 @@ class Crc32c {
                               uint32_t* d_out, void* hip_stream = nullptr) {
     return annety_crc32_batch_var(d_base, d_off, d_len, n, d_out, hip_stream);
   }
+  // Device-resident variable-length batch whose payloads lie in [d_arena, d_arena + arena_bytes) and
+  // mostly cover it (a received stream, a packed batch): one pass over the buffer.
+  static int crc32_long_batch_arena(const void* d_arena, size_t arena_bytes, const uint64_t* d_off,
+                                    const uint32_t* d_len, size_t n, uint32_t* d_out, void* hip_stream = nullptr) {
+    return annety_crc32_batch_var_arena(d_arena, arena_bytes, d_off, d_len, n, d_out, hip_stream);
+  }
+  // crc32_update over a batch: d_state[i] advanced over fragment i (fixed stride, or offsets/lengths).
+  static int crc32_update_batch(uint32_t* d_state, const void* d_base, size_t n, size_t len, size_t stride,
+                                void* hip_stream = nullptr) {
+    return annety_crc32_update_batch_fixed(d_state, d_base, n, len, stride, hip_stream);
+  }
+  static int crc32_update_batch(uint32_t* d_state, const void* d_base, const uint64_t* d_off, const uint32_t* d_len,
+                                size_t n, void* hip_stream = nullptr) {
+    return annety_crc32_update_batch_var(d_state, d_base, d_off, d_len, n, hip_stream);
+  }
   // Host-memory batch (staged H2D -> kernel -> D2H); synchronous.
   static int crc32_long_batch_host(const void* h_base, size_t n, size_t len, size_t stride, uint32_t* h_out) {
     return annety_crc32_batch_fixed_host(h_base, n, len, stride, h_out);
