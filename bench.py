@@ -87,8 +87,25 @@ def spawn(n: int, argv=None) -> int:
         env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         procs.append(subprocess.Popen([sys.executable] + list(argv), env=env,
                                       stdout=None if r == 0 else subprocess.DEVNULL))
-    rcs = [p.wait() for p in procs]
-    return max(rcs, key=lambda c: abs(c))
+    # fail fast: a rank that dies leaves the others blocked in a collective, so the first non-zero exit
+    # terminates the rest (the processes started here, by PID)
+    while True:
+        rcs = [p.poll() for p in procs]
+        if all(rc is not None for rc in rcs):
+            return max(rcs, key=lambda c: abs(c))
+        if any(rc not in (None, 0) for rc in rcs):
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            deadline = time.time() + 10
+            for p in procs:
+                try:
+                    p.wait(timeout=max(0.1, deadline - time.time()))
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            return max((p.returncode for p in procs), key=lambda c: abs(c))
+        time.sleep(0.2)
 
 
 def zipf_batch(seed: int, target: int = 1 << 30):

@@ -7,6 +7,7 @@ distributed plumbing, not the kernel (the kernel's parity is tests/test_gpu_*.py
 import os
 import socket
 import subprocess
+import time
 import sys
 
 import numpy as np
@@ -141,6 +142,10 @@ def test_bench_spawns_ranks(tmp_path):
     assert out.returncode == 0
     assert out.stdout.split() == ["0", "0", "3", "127.0.0.1"]  # rank 0's stdout only
     assert bench.spawn(2, ["-c", "import sys; sys.exit(3)"]) == 3
+    # a rank that dies ends the run: the survivor (blocked as in a collective) is terminated
+    t0 = time.time()
+    rc = bench.spawn(2, ["-c", "import os, sys, time\nif os.environ['RANK'] == '1': sys.exit(5)\ntime.sleep(600)"])
+    assert rc != 0 and time.time() - t0 < 60
 
 
 def test_shard_range_covers():
