@@ -25,6 +25,7 @@ from .crc32c import (  # noqa: F401
     PinnedHostBuffer,
     StreamingCrc,
     digests_to_numpy,
+    reserve_cus,
     tables,
 )
 from ._lib import CrcError, lib_path  # noqa: F401
@@ -41,6 +42,7 @@ __all__ = [
     "crc32_batch_host",
     "crc32_combine",
     "digests_to_numpy",
+    "reserve_cus",
     "tables",
     "LengthHeaderCodec",
     "ProtobufCodecFrames",

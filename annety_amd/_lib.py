@@ -21,6 +21,7 @@ SIGNATURES = [
     ("annety_crc_shutdown", ctypes.c_int, []),
     ("annety_crc_strerror", ctypes.c_char_p, [ctypes.c_int]),
     ("annety_crc_last_hip_error", ctypes.c_int, []),
+    ("annety_crc_reserve_cus", ctypes.c_int, [ctypes.c_int]),
     ("annety_crc32_long", _u32, [_vp, _c_size]),
     ("annety_crc32_short", _u32, [_vp, _c_size]),
     ("annety_crc32_update", None, [ctypes.POINTER(_u32), _vp, _c_size]),

@@ -75,6 +75,12 @@ def crc32_combine(crc_a: int, crc_b: int, len_b: int) -> int:
     return int(_lib.get().annety_crc32_combine(crc_a & 0xFFFFFFFF, crc_b & 0xFFFFFFFF, len_b))
 
 
+def reserve_cus(n: int) -> None:
+    """Leave n CUs of every device free of the batch kernels (annety_crc_reserve_cus), e.g. for the RCCL
+    kernels of a gather that overlaps the next chunk's checksums; 0 uses every CU."""
+    _lib.check(_lib.get().annety_crc_reserve_cus(int(n)), "annety_crc_reserve_cus")
+
+
 def tables() -> tuple[np.ndarray, np.ndarray]:
     """The drop-in's annety::internal::crc32_table256/16 (src/Crc32c.cc:20-92)."""
     lib = _lib.get()

@@ -335,6 +335,10 @@ struct DeviceCtx {
 
 constexpr int kMaxDev = 64;
 DeviceCtx g_dev[kMaxDev];
+// CUs left free by the batch kernels (annety_crc_reserve_cus): room for work on other streams, e.g. the
+// RCCL kernels of a digest gather that runs beside the next chunk's checksums
+std::atomic<int> g_reserved_cus{0};
+size_t grid_cus(const DeviceCtx& c) { return (size_t)std::max(1, c.cus - g_reserved_cus.load()); }
 std::mutex g_init_mu;
 
 int init_device_locked(int dev) {
@@ -422,7 +426,7 @@ int run_fixed(DeviceCtx& c, const void* d_base, size_t n, size_t len, size_t str
     std::memcpy(a.raw_shift_cols.c, m.col, sizeof m.col);
   }
   a.out = d_out;
-  a.max_blocks = (size_t)c.cus;
+  a.max_blocks = grid_cus(c);
   HIP_TRY(launch_fixed(a, stream));
   return ANNETY_CRC_OK;
 }
@@ -443,7 +447,7 @@ int run_var(DeviceCtx& c, const void* d_base, size_t n, uint64_t fstride, uint32
   a.img_unshift = c.d_unshift;
   a.short_init = c.d_short;
   a.out = d_out;
-  a.max_blocks = (size_t)c.cus;
+  a.max_blocks = grid_cus(c);
   HIP_TRY(launch_var(a, stream));
   return ANNETY_CRC_OK;
 }
@@ -481,7 +485,7 @@ void arena_fill(const DeviceCtx& c, const void* d_base, size_t arena_bytes, Aren
   a.img_sb = c.d_sb;
   a.img_stitch = c.d_stitch;
   a.zero_line = c.d_zero;
-  a.max_blocks = (size_t)c.cus;
+  a.max_blocks = grid_cus(c);
   if (!arena_bytes) return;
   a.byte_lo = (uint64_t)(uintptr_t)d_base;
   a.byte_hi = a.byte_lo + arena_bytes;
@@ -728,6 +732,12 @@ const char* annety_crc_strerror(int status) {
 }
 
 int annety_crc_last_hip_error(void) { return t_last_hip; }
+
+int annety_crc_reserve_cus(int n) {
+  if (n < 0) return ANNETY_CRC_EINVAL;
+  g_reserved_cus.store(n);
+  return ANNETY_CRC_OK;
+}
 
 // include/Crc32c.h:58-69
 uint32_t annety_crc32_long(const char* buff, size_t len) {

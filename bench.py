@@ -57,6 +57,12 @@ def parse():
                    help="config 3: arena = one pass over the packed arena + per-payload stitch (annety_crc32_batch_var_arena); "
                         "sorted = the general length-bucketed path (annety_crc32_batch_var)")
     p.add_argument("--chunks", type=int, default=8, help="config 4: chunks per shard for the pipelined gather")
+    p.add_argument("--dist", action="store_true",
+                   help="run the N>1 code path (RCCL process group, pipelined digest gather, gather check, max over "
+                        "ranks) even at one rank: a one-GPU rehearsal of the multi-GPU run")
+    p.add_argument("--reserve-cus", type=int, default=None,
+                   help="N>1: CUs left free of the checksum kernels for the overlapped RCCL gather "
+                        "(annety_crc_reserve_cus; default 8 when gathering, else 0)")
     p.add_argument("--payloads", type=int, default=None, help="override payloads per GPU (fixed configs)")
     p.add_argument("--len", type=int, default=None, help="override payload bytes (fixed configs)")
     p.add_argument("--e2e", action="store_true",
@@ -338,8 +344,9 @@ def main():
     if world == 0 and args.gpus > 1:
         return spawn(args.gpus)  # before anything touches the GPU
     world = max(world, 1)
+    multi = world > 1 or args.dist  # the distributed code path
     if args.config is None:
-        args.config = 4 if world > 1 else 1
+        args.config = 4 if multi else 1
 
     import torch
     import torch.distributed as dist
@@ -348,16 +355,26 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    if world > 1:
+    if multi:
+        if world == 1:
+            os.environ.setdefault("RANK", "0")
+            os.environ.setdefault("WORLD_SIZE", "1")
+            os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", str(_free_port()))
         dist.init_process_group("nccl", device_id=dev)
 
     import oracle
     from annety_amd import sharded
 
+    import annety_amd
+
+    # the checksum kernels take one workgroup per CU; with the gather overlapped on another stream, a few
+    # free CUs let the RCCL kernels run beside them instead of between chunks
+    annety_amd.reserve_cus(args.reserve_cus if args.reserve_cus is not None else (8 if multi else 0))
     w = Workload(args, dev, rank)
     stream = torch.cuda.current_stream(dev)
     sh = int(stream.cuda_stream)
-    pipe = sharded.PipelinedGather(w.n, args.chunks, dst=0, device=dev) if world > 1 else None
+    pipe = sharded.PipelinedGather(w.n, args.chunks, dst=0, device=dev) if multi else None
 
     def step(gather: bool = True):
         if pipe is None:
@@ -379,17 +396,17 @@ def main():
         raise SystemExit(f"rank {rank}: gathered digests differ from the ranks' own")
 
     def timed(steps: int, gather: bool) -> float:
-        if world > 1:
+        if multi:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         for _ in range(steps):
             sharded.PipelinedGather.wait(step(gather))
         torch.cuda.synchronize()
-        if world > 1:
+        if multi:
             dist.barrier()
         el = time.perf_counter() - t0
-        if world > 1:  # max over ranks
+        if multi:  # max over ranks
             t = torch.tensor([el], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
@@ -414,7 +431,7 @@ def main():
     kern_ms = ev0.elapsed_time(ev1) / args.steps
 
     elapsed = timed(args.steps, gather=True)
-    compute_only = timed(args.steps, gather=False) if world > 1 else None
+    compute_only = timed(args.steps, gather=False) if multi else None
 
     if rank == 0:
         total_gib = w.payload_bytes * world * args.steps / 2 ** 30
@@ -438,7 +455,7 @@ def main():
                 "payloads_per_gpu": w.n,
                 "payload_bytes": w.L if w.L else "zipf",
                 "bytes_per_gpu": w.payload_bytes,
-                "parallelism": f"shard{world}" if world > 1 else "single",
+                "parallelism": f"shard{world}" if multi else "single",
             },
             "roofline": {
                 "bound": "hbm",
@@ -451,9 +468,9 @@ def main():
                 "kernel_ms_avg": round(kern_ms, 4),
                 "algorithmic_bytes_per_launch": w.algo_bytes,
             },
-            "cpu_baseline": None if (args.no_cpu or world > 1) else cpu_baseline(hs, ho, hl, args.cpu_seconds),
+            "cpu_baseline": None if (args.no_cpu or multi) else cpu_baseline(hs, ho, hl, args.cpu_seconds),
         }
-        if world > 1:
+        if multi:
             line["rccl_ranks"] = dist.get_world_size()
             line["backend"] = dist.get_backend()
             line["gather"] = {"chunks": len(pipe.bounds), "bytes_to_rank0_per_step": 4 * w.n * (world - 1),
@@ -462,7 +479,7 @@ def main():
         if args.e2e and world == 1:
             line["e2e_host_path"] = e2e_host_path(w)
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if multi:
         dist.destroy_process_group()
     return 0
 

@@ -45,6 +45,10 @@ int annety_crc_shutdown(void);
 const char* annety_crc_strerror(int status);
 /* Last hipError_t seen by this thread (0 if none). */
 int annety_crc_last_hip_error(void);
+/* Leave n CUs of every device free of the batch kernels (which otherwise take one workgroup per CU), so
+ * that work on other streams - e.g. the RCCL kernels of a digest gather overlapped with the next chunk -
+ * runs beside them instead of between them. 0 (default) uses every CU. Process-wide. */
+int annety_crc_reserve_cus(int n);
 
 /* ---- host scalar API: exact replacements of the reference's inline methods ----
  * annety_crc32_long   replaces Crc32c::crc32_long(const char*, size_t)   include/Crc32c.h:58-69
