@@ -54,10 +54,22 @@ def gather_digests(local: torch.Tensor, counts: Sequence[int], dst: int = 0, gro
     return torch.cat([p[:c] for p, c in zip(parts, counts)])
 
 
-def chunk_bounds(n: int, chunks: int) -> List[tuple]:
-    """[lo, hi) of `chunks` near-equal consecutive pieces of n payloads (empty pieces dropped)."""
+def chunk_bounds(n: int, chunks: int, taper: int = 0) -> List[tuple]:
+    """[lo, hi) of `chunks` near-equal consecutive pieces of n payloads (empty pieces dropped). With
+    `taper` t > 0 the last piece is cut again into t pieces of 1/2, 1/4, ..., 1/2^(t-1), 1/2^(t-1) of it:
+    in a pipelined gather only the last piece's transfer is not hidden behind compute."""
     chunks = max(1, min(chunks, n)) if n else 1
-    return [(n * k // chunks, n * (k + 1) // chunks) for k in range(chunks) if n * (k + 1) // chunks > n * k // chunks]
+    b = [(n * k // chunks, n * (k + 1) // chunks) for k in range(chunks) if n * (k + 1) // chunks > n * k // chunks]
+    if taper > 1 and b:
+        lo, hi = b.pop()
+        for _ in range(taper - 1):
+            if hi - lo < 2:
+                break
+            mid = hi - (hi - lo) // 2
+            b.append((lo, mid))
+            lo = mid
+        b.append((lo, hi))
+    return b
 
 
 class PipelinedGather:
@@ -68,11 +80,12 @@ class PipelinedGather:
     torch.distributed issues each collective on its communication stream after the work already queued
     on the current stream, so `produce` (a kernel launch) and the gathers overlap with no extra sync."""
 
-    def __init__(self, n_local: int, chunks: int, dst: int = 0, group=None, device=None, dtype=torch.int32):
+    def __init__(self, n_local: int, chunks: int, dst: int = 0, group=None, device=None, dtype=torch.int32,
+                 taper: int = 0):
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.dst, self.group = dst, group
-        self.bounds = chunk_bounds(n_local, chunks)
+        self.bounds = chunk_bounds(n_local, chunks, taper)
         self.recv = (torch.empty((self.world, n_local), dtype=dtype, device=device) if self.rank == dst else None)
 
     def run(self, produce: Callable[[int, int], torch.Tensor], gather: bool = True):

@@ -57,12 +57,20 @@ def parse():
                    help="config 3: arena = one pass over the packed arena + per-payload stitch (annety_crc32_batch_var_arena); "
                         "sorted = the general length-bucketed path (annety_crc32_batch_var)")
     p.add_argument("--chunks", type=int, default=8, help="config 4: chunks per shard for the pipelined gather")
+    p.add_argument("--hw-queues", type=int, default=8,
+                   help="N>1: raise GPU_MAX_HW_QUEUES to this (<= 32) so the compute and RCCL streams get queues of "
+                        "their own")
+    p.add_argument("--taper", type=int, default=0,
+                   help="config 4: cut the last chunk into this many halving pieces (only the last piece's gather "
+                        "is not hidden behind compute); 0 = equal chunks")
     p.add_argument("--dist", action="store_true",
                    help="run the N>1 code path (RCCL process group, pipelined digest gather, gather check, max over "
                         "ranks) even at one rank: a one-GPU rehearsal of the multi-GPU run")
     p.add_argument("--reserve-cus", type=int, default=None,
                    help="N>1: CUs left free of the checksum kernels for the overlapped RCCL gather "
                         "(annety_crc_reserve_cus; default 8 when gathering, else 0)")
+    p.add_argument("--compute-stream", choices=["default", "own"], default="default",
+                   help="launch the checksum kernels on torch's default stream or on a stream of their own")
     p.add_argument("--payloads", type=int, default=None, help="override payloads per GPU (fixed configs)")
     p.add_argument("--len", type=int, default=None, help="override payload bytes (fixed configs)")
     p.add_argument("--e2e", action="store_true",
@@ -159,7 +167,8 @@ class Workload:
                 self.kernel = "crc32_oneround_kernel<8> (annety_amd/csrc/crc32_kernels.hip)"
             if args.config == 4:
                 self.desc = (f"BASELINE config 4 shard: {n} x {L} B payloads per GPU (64M x 1 KiB at 8 GPUs), "
-                             f"{args.chunks} chunks per step, each chunk's digests gathered to rank 0 over RCCL "
+                             f"{args.chunks} chunks per step (the last cut into {args.taper} halving pieces), each chunk's "
+                             "digests gathered to rank 0 over RCCL "
                              "while the next chunk is computed")
             else:
                 self.desc = (f"BASELINE config {args.config}: {n} x {L} B payloads contiguous in HBM per GPU, "
@@ -347,6 +356,11 @@ def main():
     multi = world > 1 or args.dist  # the distributed code path
     if args.config is None:
         args.config = 4 if multi else 1
+    if multi and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < args.hw_queues:
+        # HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default); the compute stream, torch's
+        # RCCL stream and RCCL's own streams then share queues, and a queue runs its packets in order. Set
+        # before HIP initialises (nothing has touched the GPU yet): one-rank rehearsal 4 -> 8 queues +4-5 %.
+        os.environ["GPU_MAX_HW_QUEUES"] = str(args.hw_queues)
 
     import torch
     import torch.distributed as dist
@@ -372,9 +386,11 @@ def main():
     # free CUs let the RCCL kernels run beside them instead of between chunks
     annety_amd.reserve_cus(args.reserve_cus if args.reserve_cus is not None else (8 if multi else 0))
     w = Workload(args, dev, rank)
+    if args.compute_stream == "own":
+        torch.cuda.set_stream(torch.cuda.Stream(dev))
     stream = torch.cuda.current_stream(dev)
     sh = int(stream.cuda_stream)
-    pipe = sharded.PipelinedGather(w.n, args.chunks, dst=0, device=dev) if multi else None
+    pipe = sharded.PipelinedGather(w.n, args.chunks, dst=0, device=dev, taper=args.taper) if multi else None
 
     def step(gather: bool = True):
         if pipe is None:

@@ -159,3 +159,11 @@ def test_shard_range_covers():
             assert max(h - l for l, h in rs) - min(h - l for l, h in rs) <= 1
     assert sharded.chunk_bounds(10, 3) == [(0, 3), (3, 6), (6, 10)]
     assert sharded.chunk_bounds(2, 8) == [(0, 1), (1, 2)]
+    # tapered tail: the last of 8 pieces cut into 1/2, 1/4, 1/4
+    b = sharded.chunk_bounds(8192, 8, taper=3)
+    assert b[:7] == [(1024 * k, 1024 * (k + 1)) for k in range(7)]
+    assert b[7:] == [(7168, 7680), (7680, 7936), (7936, 8192)]
+    for n, c, t in [(1, 8, 3), (5, 2, 4), (1000, 7, 3), (10 ** 6 + 3, 8, 5)]:
+        b = sharded.chunk_bounds(n, c, taper=t)
+        assert b[0][0] == 0 and b[-1][1] == n and all(lo < hi for lo, hi in b)
+        assert all(b[i][1] == b[i + 1][0] for i in range(len(b) - 1))
