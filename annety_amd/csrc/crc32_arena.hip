@@ -323,7 +323,8 @@ __device__ __forceinline__ LaneCtx lane_ctx() {
 
 // Second launch of the two-launch path: contiguous payload ranges per block (coalesced descriptor loads),
 // the same count for every block; the first payload's loads are in flight while the LDS image is staged.
-template <bool UPD, int BLK = kStitchBlock, int PROBE = 0>
+//   PIPE (microbench A/B): 1 = the next payload's loads are issued before the current one is folded.
+template <bool UPD, int BLK = kStitchBlock, int PROBE = 0, int PIPE = 0>
 __global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchGeo g, const uint4* __restrict__ img_slice,
                                                                  const uint4* __restrict__ img_stitch) {
   __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsStitchImageBytes / 16];
@@ -337,14 +338,38 @@ __global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchGeo g, co
     st.plan_a(p_first, y, v);
     st.plan_b(p_first, y, v);
   }
-  load_image<kLdsStitchImageBytes, BLK, kLdsCommonBytes>(lds4, img_slice, nullptr, img_stitch);
-  __syncthreads();
-  for (size_t p = p_first; p < p_end; p += BLK) {
-    if (p != p_first) {
-      st.plan_a(p, y, v);
-      st.plan_b(p, y, v);
+  if constexpr (PIPE == 1) {
+    Plan y2{};
+    Vals v2{};
+    if (p_first + BLK < p_end) {
+      st.plan_a(p_first + BLK, y2, v2);
+      st.plan_b(p_first + BLK, y2, v2);
     }
-    st.process(p, y, v);
+    load_image<kLdsStitchImageBytes, BLK, kLdsCommonBytes>(lds4, img_slice, nullptr, img_stitch);
+    __syncthreads();
+    // (y, v) holds payload p, (y2, v2) payload p + BLK; each refills while the other folds
+    for (size_t p = p_first; p < p_end; p += 2 * BLK) {
+      st.process(p, y, v);
+      if (p + 2 * BLK < p_end) {
+        st.plan_a(p + 2 * BLK, y, v);
+        st.plan_b(p + 2 * BLK, y, v);
+      }
+      if (p + BLK < p_end) st.process(p + BLK, y2, v2);
+      if (p + 3 * BLK < p_end) {
+        st.plan_a(p + 3 * BLK, y2, v2);
+        st.plan_b(p + 3 * BLK, y2, v2);
+      }
+    }
+  } else {
+    load_image<kLdsStitchImageBytes, BLK, kLdsCommonBytes>(lds4, img_slice, nullptr, img_stitch);
+    __syncthreads();
+    for (size_t p = p_first; p < p_end; p += BLK) {
+      if (p != p_first) {
+        st.plan_a(p, y, v);
+        st.plan_b(p, y, v);
+      }
+      st.process(p, y, v);
+    }
   }
 }
 
@@ -407,17 +432,17 @@ StitchGeo stitch_geo(const ArenaLaunch& a, const ArenaGeom& geo) {
   return s;
 }
 
-template <int PROBE>
+template <int PROBE, int PIPE = 0>
 hipError_t launch_stitch_p(const ArenaLaunch& a, hipStream_t stream) {
   const StitchGeo s = stitch_geo(a, arena_geom(a));
   const size_t blocks = stitch_blocks(a);
   const uint4* img_slice = static_cast<const uint4*>(a.img_slice);
   const uint4* img_stitch = static_cast<const uint4*>(a.img_stitch);
   if (a.update)
-    hipLaunchKernelGGL((crc32_arena_stitch_kernel<true, kStitchBlock, PROBE>), dim3((unsigned)blocks),
+    hipLaunchKernelGGL((crc32_arena_stitch_kernel<true, kStitchBlock, PROBE, PIPE>), dim3((unsigned)blocks),
                        dim3(kStitchBlock), 0, stream, s, img_slice, img_stitch);
   else
-    hipLaunchKernelGGL((crc32_arena_stitch_kernel<false, kStitchBlock, PROBE>), dim3((unsigned)blocks),
+    hipLaunchKernelGGL((crc32_arena_stitch_kernel<false, kStitchBlock, PROBE, PIPE>), dim3((unsigned)blocks),
                        dim3(kStitchBlock), 0, stream, s, img_slice, img_stitch);
   return hipGetLastError();
 }

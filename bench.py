@@ -56,13 +56,19 @@ def parse():
     p.add_argument("--var-path", choices=["arena", "sorted"], default="arena",
                    help="config 3: arena = one pass over the packed arena + per-payload stitch (annety_crc32_batch_var_arena); "
                         "sorted = the general length-bucketed path (annety_crc32_batch_var)")
-    p.add_argument("--chunks", type=int, default=8, help="config 4: chunks per shard for the pipelined gather")
+    p.add_argument("--chunks", type=int, default=2,
+                   help="config 4: chunks per shard for the pipelined gather (one-rank rehearsal with the cross-step "
+                        "overlap, one box: 1/2/4 chunks 5755-5770/5748/5613-5616 GiB/s, profiles/r02/config4_chunks_overlap.log)")
     p.add_argument("--hw-queues", type=int, default=8,
                    help="N>1: raise GPU_MAX_HW_QUEUES to this (<= 32) so the compute and RCCL streams get queues of "
                         "their own")
     p.add_argument("--taper", type=int, default=0,
                    help="config 4: cut the last chunk into this many halving pieces (only the last piece's gather "
                         "is not hidden behind compute); 0 = equal chunks")
+    p.add_argument("--no-overlap-steps", action="store_true",
+                   help="config 4: wait for a step's gathers before the next step starts (default: the digests "
+                        "alternate between two buffers and step s+1's chunks compute while step s's last gathers "
+                        "are in flight; every gather is still inside the timed region)")
     p.add_argument("--dist", action="store_true",
                    help="run the N>1 code path (RCCL process group, pipelined digest gather, gather check, max over "
                         "ranks) even at one rank: a one-GPU rehearsal of the multi-GPU run")
@@ -169,7 +175,9 @@ class Workload:
                 self.desc = (f"BASELINE config 4 shard: {n} x {L} B payloads per GPU (64M x 1 KiB at 8 GPUs), "
                              f"{args.chunks} chunks per step (the last cut into {args.taper} halving pieces), each chunk's "
                              "digests gathered to rank 0 over RCCL "
-                             "while the next chunk is computed")
+                             "while the next chunk is computed" +
+                             ("" if args.no_overlap_steps else
+                              " (digests double-buffered: the next step computes while this step's last gathers finish)"))
             else:
                 self.desc = (f"BASELINE config {args.config}: {n} x {L} B payloads contiguous in HBM per GPU, "
                              "one batch launch per step")
@@ -392,11 +400,30 @@ def main():
     sh = int(stream.cuda_stream)
     pipe = sharded.PipelinedGather(w.n, args.chunks, dst=0, device=dev, taper=args.taper) if multi else None
 
+    # N>1: the digests alternate between two buffers, so step s+1's chunks can be computed while step s's
+    # last gathers still read the other buffer; a step's handles are waited (the compute stream waits for
+    # its gathers, no host block) after the next step is launched, before the buffer comes round again
+    outs = [w.out, torch.empty_like(w.out)] if (pipe is not None and not args.no_overlap_steps) else [w.out]
+    nstep = [0]
+
     def step(gather: bool = True):
         if pipe is None:
             w.launch(sh)
             return []
+        w.out = outs[nstep[0] % len(outs)]
+        nstep[0] += 1
         return pipe.run(lambda lo, hi: w.launch(sh, lo, hi), gather=gather)
+
+    def run_steps(steps: int, gather: bool) -> None:
+        prev = []
+        for _ in range(steps):
+            h = step(gather)
+            if len(outs) > 1:
+                sharded.PipelinedGather.wait(prev)
+                prev = h
+            else:
+                sharded.PipelinedGather.wait(h)
+        sharded.PipelinedGather.wait(prev)
 
     # correctness gate before timing: bit-exact vs the oracle on a prefix of this rank's batch, and (N > 1)
     # every rank's digests delivered to rank 0 intact (checksum of checksums)
@@ -416,8 +443,7 @@ def main():
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        for _ in range(steps):
-            sharded.PipelinedGather.wait(step(gather))
+        run_steps(steps, gather)
         torch.cuda.synchronize()
         if multi:
             dist.barrier()
@@ -433,8 +459,7 @@ def main():
         for _ in range(10 if world == 1 else 1):
             step(gather=False)
         torch.cuda.synchronize()
-    for _ in range(args.warmup):
-        sharded.PipelinedGather.wait(step())
+    run_steps(args.warmup, True)
     torch.cuda.synchronize()
 
     # kernel-only time on the launch stream (HIP events around the same number of steps, no gather)
@@ -490,7 +515,8 @@ def main():
             line["rccl_ranks"] = dist.get_world_size()
             line["backend"] = dist.get_backend()
             line["gather"] = {"chunks": len(pipe.bounds), "bytes_to_rank0_per_step": 4 * w.n * (world - 1),
-                              "verified": bool(gather_ok), "overlapped_with_compute": True}
+                              "verified": bool(gather_ok), "overlapped_with_compute": True,
+                              "overlapped_across_steps": len(outs) > 1}
             line["value_compute_only"] = round(total_gib / compute_only, 2)
         if args.e2e and world == 1:
             line["e2e_host_path"] = e2e_host_path(w)
