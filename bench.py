@@ -82,6 +82,9 @@ def parse():
     p.add_argument("--e2e", action="store_true",
                    help="also time the host-memory path (pinned staging, H2D -> kernel -> D2H) on the same batch")
     p.add_argument("--no-cpu", action="store_true", help="skip the cpu_baseline leg")
+    p.add_argument("--sample-check", action="store_true",
+                   help="check only a 4 MiB prefix of the batch against the oracle before timing (default: every "
+                        "digest, 1 GiB at a time)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample duration")
     return p.parse_args()
 
@@ -223,6 +226,31 @@ class Workload:
         ns = max(1, int(np.searchsorted(end, max_bytes)))
         h = self.data[: int(end[ns - 1])].cpu().numpy()
         return h, offs[:ns].astype(np.uint64), lens[:ns].astype(np.uint32)
+
+
+def full_check(w: Workload, threads: int) -> dict:
+    """Every digest of the batch against the oracle (C restatement, pinned by tests/golden), 1 GiB of
+    payloads at a time so host memory stays bounded (config 2: 16 GiB in 16 pieces)."""
+    import oracle
+
+    t0 = time.perf_counter()
+    if w.config in (1, 2, 4):
+        per = max(1, (1 << 30) // w.L)
+        for lo in range(0, w.n, per):
+            hi = min(w.n, lo + per)
+            h = w.data[lo * w.L:hi * w.L].cpu().numpy()
+            got = w.out[lo:hi].cpu().numpy().view(np.uint32)
+            want = oracle.batch_fixed_mt(h, hi - lo, w.L, threads=threads)
+            if not np.array_equal(got, want):
+                raise SystemExit(f"digest of payload {int(np.flatnonzero(got != want)[0]) + lo} differs from the oracle")
+    else:
+        h = w.data.cpu().numpy()
+        want = oracle.batch_var_mt(h, w.offsets.cpu().numpy().astype(np.uint64),
+                                   w.lengths.cpu().numpy().astype(np.uint32), threads=threads)
+        if not np.array_equal(w.out.cpu().numpy().view(np.uint32), want):
+            raise SystemExit("digests differ from the oracle")
+    return {"payloads": w.n, "against": "oracle (C restatement pinned by tests/golden)", "threads": threads,
+            "seconds": round(time.perf_counter() - t0, 2)}
 
 
 def cpu_baseline(h: np.ndarray, offs: np.ndarray, lens: np.ndarray, budget_s: float) -> dict:
@@ -434,6 +462,7 @@ def main():
     got = w.out[: len(ho)].cpu().numpy().view(np.uint32)
     if not np.array_equal(got, want):
         raise SystemExit(f"rank {rank}: digests differ from the oracle on the sample")
+    checked = full_check(w, threads=min(16, os.cpu_count() or 1)) if not args.sample_check else None
     gather_ok = sharded.verify_gather(pipe.recv, w.out) if pipe is not None else None
     if gather_ok is False:
         raise SystemExit(f"rank {rank}: gathered digests differ from the ranks' own")
@@ -510,6 +539,7 @@ def main():
                 "algorithmic_bytes_per_launch": w.algo_bytes,
             },
             "cpu_baseline": None if (args.no_cpu or multi) else cpu_baseline(hs, ho, hl, args.cpu_seconds),
+            "checked_vs_oracle": checked,
         }
         if multi:
             line["rccl_ranks"] = dist.get_world_size()

@@ -40,3 +40,23 @@ def test_group_host_batch(gpu):
     with sharded.DeviceGroup([0]) as g:
         got = g.batch_fixed_host(host, n, L)
     assert np.array_equal(got, oracle.batch_fixed_mt(host, n, L, threads=8))
+
+
+def test_bench_dist_path_one_rank(gpu):
+    """bench.py's N > 1 code path at one rank over RCCL (--dist): the real kernels produce each chunk,
+    the digests (double-buffered across steps) are gathered asynchronously, the correctness gate checks
+    the rank's digests against the oracle and verify_gather checks what rank 0 received."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--dist", "--config", "4", "--payloads", "65536",
+           "--steps", "4", "--warmup", "2", "--prewarm-s", "0", "--chunks", "3"]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=root)
+    assert r.returncode == 0, r.stderr[-2000:]
+    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["rccl_ranks"] == 1 and line["backend"] == "nccl"
+    assert line["gather"]["verified"] is True and line["gather"]["overlapped_across_steps"] is True
+    assert line["gather"]["chunks"] == 3 and line["n_gpus"] == 1 and line["value"] > 0
