@@ -104,6 +104,23 @@ class PipelinedGather:
         for h in handles:
             h.wait()
 
+    def run_steps(self, produce: Callable[[int, int, int], torch.Tensor], steps: int, buffers: int = 2,
+                  gather: bool = True) -> None:
+        """`steps` consecutive steps; produce(s, lo, hi) writes step s's digests of [lo, hi) into buffer
+        s % buffers and returns that view. With two buffers, step s's handles are waited only after step
+        s+1 is launched (on a GPU: the compute stream waits for step s's gathers, no host block), so step
+        s+1 computes while step s's last gathers still read the other buffer; the buffer step s+2 reuses
+        is free by then. Everything is waited before returning."""
+        prev = []
+        for s in range(steps):
+            h = self.run(lambda lo, hi, s=s: produce(s, lo, hi), gather=gather)
+            if buffers > 1:
+                self.wait(prev)
+                prev = h
+            else:
+                self.wait(h)
+        self.wait(prev)
+
 
 def digest_checksum(t: torch.Tensor) -> int:
     """CRC-32 of a digest array's bytes (a checksum of checksums, computed on the host)."""

@@ -442,16 +442,16 @@ def main():
         nstep[0] += 1
         return pipe.run(lambda lo, hi: w.launch(sh, lo, hi), gather=gather)
 
+    def produce(s: int, lo: int, hi: int):
+        w.out = outs[s % len(outs)]
+        return w.launch(sh, lo, hi)
+
     def run_steps(steps: int, gather: bool) -> None:
-        prev = []
-        for _ in range(steps):
-            h = step(gather)
-            if len(outs) > 1:
-                sharded.PipelinedGather.wait(prev)
-                prev = h
-            else:
-                sharded.PipelinedGather.wait(h)
-        sharded.PipelinedGather.wait(prev)
+        if pipe is None:
+            for _ in range(steps):
+                w.launch(sh)
+        else:
+            pipe.run_steps(produce, steps, buffers=len(outs), gather=gather)
 
     # correctness gate before timing: bit-exact vs the oracle on a prefix of this rank's batch, and (N > 1)
     # every rank's digests delivered to rank 0 intact (checksum of checksums)

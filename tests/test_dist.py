@@ -129,6 +129,60 @@ def test_gloo_world2_pipelined_gather(corrupt):
         assert recv[r] == want
 
 
+def _steps_worker(rank, world, port, n_local, L, chunks, steps, buffers, q):
+    """bench.py's timed loop at N > 1 (PipelinedGather.run_steps): every step's digests differ (a
+    different shard per step), written into buffer s % buffers; rank 0 logs what it received after each
+    step's gathers are waited, which with two buffers is one step later."""
+    import torch.distributed as dist
+
+    from annety_amd import sharded
+
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        outs = [torch.zeros(n_local, dtype=torch.int32) for _ in range(buffers)]
+        pipe = sharded.PipelinedGather(n_local, chunks, dst=0)
+
+        def produce(s, lo, hi):
+            arena = oracle.lcg_bytes(n_local * L, 100 * s + rank)
+            out = outs[s % buffers]
+            out[lo:hi] = torch.from_numpy(oracle.batch_fixed(arena[lo * L:hi * L], hi - lo, L).view(np.int32).copy())
+            return out[lo:hi]
+
+        pipe.run_steps(produce, steps, buffers=buffers)
+        if rank == 0:
+            q.put(("recv", pipe.recv.numpy().view(np.uint32).tolist()))
+        # every buffer still holds its last step's digests (no step overwrote a buffer under a gather)
+        for b in range(buffers):
+            s = max(x for x in range(steps) if x % buffers == b)
+            want = oracle.batch_fixed(oracle.lcg_bytes(n_local * L, 100 * s + rank), n_local, L)
+            q.put(("buf", rank, b, bool(np.array_equal(outs[b].numpy().view(np.uint32), want))))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("buffers", [1, 2])
+def test_gloo_world2_run_steps(buffers):
+    n_local, L, chunks, steps = 600, 128, 3, 5
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_steps_worker, args=(r, 2, port, n_local, L, chunks, steps, buffers, q))
+             for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(120)
+        assert p.exitcode == 0
+    msgs = [q.get(timeout=5) for _ in range(1 + 2 * buffers)]
+    assert all(m[3] for m in msgs if m[0] == "buf")
+    recv = [m for m in msgs if m[0] == "recv"][0][1]
+    for r in range(2):  # rank 0 ends holding the last step's digests of every rank
+        want = oracle.batch_fixed(oracle.lcg_bytes(n_local * L, 100 * (steps - 1) + r), n_local, L).tolist()
+        assert recv[r] == want
+
+
 def test_bench_spawns_ranks(tmp_path):
     """bench.py --gpus N without a launcher starts N ranks with the torchrun environment."""
     sys.path.insert(0, ROOT)
