@@ -152,9 +152,10 @@ struct Stitcher {
   }
 
   // Phase A: descriptor, plan, window and register loads (nothing the line pass writes).
-  __device__ __forceinline__ void plan_a(size_t p, Plan& y, Vals& v) const {
-    y.len = g.len[p];
-    y.A = (uint64_t)(uintptr_t)g.base + g.off[p];
+  __device__ __forceinline__ void plan_a(size_t p, Plan& y, Vals& v) const { plan_a(p, g.len[p], g.off[p], y, v); }
+  __device__ __forceinline__ void plan_a(size_t p, uint32_t len, uint64_t off, Plan& y, Vals& v) const {
+    y.len = len;
+    y.A = (uint64_t)(uintptr_t)g.base + off;
     y.E = y.A + y.len;
     y.fast = y.len > 0 && y.A >= g.byte_lo && y.E <= g.byte_hi;
     const uint64_t L0 = y.A >> 7, L1 = (y.E - (y.len ? 1 : 0)) >> 7;
@@ -323,7 +324,8 @@ __device__ __forceinline__ LaneCtx lane_ctx() {
 
 // Second launch of the two-launch path: contiguous payload ranges per block (coalesced descriptor loads),
 // the same count for every block; the first payload's loads are in flight while the LDS image is staged.
-//   PIPE (microbench A/B): 1 = the next payload's loads are issued before the current one is folded.
+//   PIPE (microbench A/B, product = 0): 1 = the next payload's loads are issued before the
+//   current one is folded; 2 = a lane's first two payloads' descriptors and plan loads issued together.
 template <bool UPD, int BLK = kStitchBlock, int PROBE = 0, int PIPE = 0>
 __global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchGeo g, const uint4* __restrict__ img_slice,
                                                                  const uint4* __restrict__ img_stitch) {
@@ -359,6 +361,30 @@ __global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchGeo g, co
         st.plan_a(p + 3 * BLK, y2, v2);
         st.plan_b(p + 3 * BLK, y2, v2);
       }
+    }
+  } else if constexpr (PIPE == 2) {
+    // the block's first two payloads per lane: both descriptors in flight together, then both plans'
+    // loads, all before the LDS image is staged. Loads are unconditional (a lane without a payload reads
+    // a valid one's) so the wait counts stay exact; the rest of a long batch runs one payload at a time.
+    const size_t last = p_end > 0 ? p_end - 1 : 0;
+    const size_t p2 = p_first + BLK;
+    const size_t q1 = p_first < p_end ? p_first : last, q2 = p2 < p_end ? p2 : last;
+    Plan y2{};
+    Vals v2{};
+    const uint32_t l1 = g.len[q1], l2 = g.len[q2];
+    const uint64_t o1 = g.off[q1], o2 = g.off[q2];
+    st.plan_a(q1, l1, o1, y, v);
+    st.plan_b(q1, y, v);
+    st.plan_a(q2, l2, o2, y2, v2);
+    st.plan_b(q2, y2, v2);
+    load_image<kLdsStitchImageBytes, BLK, kLdsCommonBytes>(lds4, img_slice, nullptr, img_stitch);
+    __syncthreads();
+    if (p_first < p_end) st.process(p_first, y, v);
+    if (p2 < p_end) st.process(p2, y2, v2);
+    for (size_t p = p2 + BLK; p < p_end; p += BLK) {
+      st.plan_a(p, y, v);
+      st.plan_b(p, y, v);
+      st.process(p, y, v);
     }
   } else {
     load_image<kLdsStitchImageBytes, BLK, kLdsCommonBytes>(lds4, img_slice, nullptr, img_stitch);

@@ -62,15 +62,18 @@ int main() {
   t([&] { CK(launch_stitch_p<2>(a, 0)); }, "  + all loads");
   t([&] { CK(launch_stitch_p<3>(a, 0)); }, "  + window folds, no map steps");
   t([&] { CK((launch_stitch_p<0, 1>(a, 0))); }, "stitch, next payload prefetched (PIPE 1)");
-  {
+  t([&] { CK((launch_stitch_p<0, 2>(a, 0))); }, "stitch, two payloads' loads together (PIPE 2)");
+  auto same = [&](auto f, const char* name) {
     std::vector<uint32_t> r0(n), r1(n);
     CK(launch_stitch_p<0>(a, 0)); CK(hipMemcpy(r0.data(), out, n * 4, hipMemcpyDeviceToHost));
     CK(hipMemset(out, 0, n * 4));
-    CK((launch_stitch_p<0, 1>(a, 0))); CK(hipMemcpy(r1.data(), out, n * 4, hipMemcpyDeviceToHost));
+    f(); CK(hipMemcpy(r1.data(), out, n * 4, hipMemcpyDeviceToHost));
     size_t bad = 0;
     for (size_t i = 0; i < n; i++) bad += r0[i] != r1[i];
-    printf("PIPE 1 vs product: %zu of %zu digests differ\n", bad, n);
-  }
+    printf("%s vs product: %zu of %zu digests differ\n", name, bad, n);
+  };
+  same([&] { CK((launch_stitch_p<0, 1>(a, 0))); }, "PIPE 1");
+  same([&] { CK((launch_stitch_p<0, 2>(a, 0))); }, "PIPE 2");
   t([&] { CK(launch_stitch_p<0>(a, 0)); }, "stitch (product, again)");
   t([&] { CK(launch_arena(a, 0)); }, "line pass + stitch (no alloc)");
   t([&] { RC(annety_crc32_batch_var_arena(d, total, doff, dlen, n, out, nullptr)); }, "product arena call (both + alloc)");
