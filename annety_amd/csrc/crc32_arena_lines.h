@@ -130,19 +130,23 @@ __device__ __forceinline__ void arena_line_pass(const uint8_t* __restrict__ base
   // next task's loads behind a branch the waitcnt pass merges the two paths and waits vmcnt(0) before
   // every fold, which serialises the A/B double buffer.
   for (int t = 0; t < ntasks; t += 2) {
+    ANNETY_PRIO_HI();
     {
       const uint4* s = reinterpret_cast<const uint4*>(t + 1 < ntasks ? lp + pstep : lp);
 #pragma unroll
       for (int i = 0; i < 8; i++) B[i] = s[i];
     }
     __builtin_amdgcn_sched_barrier(0);
+    ANNETY_PRIO_LO();
     finish(absorb_line(0u, A, k, lds), t);
+    ANNETY_PRIO_HI();
     {
       const uint4* s = reinterpret_cast<const uint4*>(t + 2 < ntasks ? lp + 2 * pstep : lp);
 #pragma unroll
       for (int i = 0; i < 8; i++) A[i] = s[i];
     }
     __builtin_amdgcn_sched_barrier(0);
+    ANNETY_PRIO_LO();
     if (t + 1 < ntasks) finish(absorb_line(0u, B, k, lds), t + 1);
     lp += 2 * pstep;
   }

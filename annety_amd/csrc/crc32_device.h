@@ -208,6 +208,16 @@ __device__ __forceinline__ uint4 gload16(uint64_t addr) {
   return make_uint4(x.x, x.y, x.z, x.w);
 }
 
+// The streaming loops raise their wave priority while they issue the next task's loads, so the
+// other wave on the SIMD (in its fold) does not delay them: config-1 kernel -0.5..1.0 %, arena line
+// pass -1.5 % (profiles/r02/setprio_ab.log; priority 3 measured the same as 1); bench steps, two passes
+// each: config 1 -0.9..-1.0 %, config 2 -0.3..-0.6 %, config 3 -0.8 % and -6.3 % (setprio_bench_ab.log).
+#ifndef ANNETY_PRIO
+#define ANNETY_PRIO 1
+#endif
+#define ANNETY_PRIO_HI() do { if constexpr (ANNETY_PRIO) __builtin_amdgcn_s_setprio(ANNETY_PRIO); } while (0)
+#define ANNETY_PRIO_LO() do { if constexpr (ANNETY_PRIO) __builtin_amdgcn_s_setprio(0); } while (0)
+
 // Keep bytes [lo8/8, hi8/8) of a line (N = 8) or half line (N = 4), zero the rest (branch-free, per
 // 32-bit word).
 template <int N>

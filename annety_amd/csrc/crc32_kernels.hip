@@ -119,19 +119,23 @@ __global__ __launch_bounds__(kBlock) void crc32_fixed_kernel(const uint8_t* __re
 
   // unconditional loads (a step past the end re-reads step 0's line): see crc32_oneround_kernel
   for (size_t q = 0; q < nsteps; q += 2) {
+    ANNETY_PRIO_HI();
     {
       const bool ok = q + 1 < nsteps;
       load_step(ok ? t_ld : 0, ok ? r_ld : 0u, B);
     }
     advance(t_ld, r_ld);
     __builtin_amdgcn_sched_barrier(0);
+    ANNETY_PRIO_LO();
     compute_step(A);
+    ANNETY_PRIO_HI();
     {
       const bool ok = q + 2 < nsteps;
       load_step(ok ? t_ld : 0, ok ? r_ld : 0u, A);
     }
     advance(t_ld, r_ld);
     __builtin_amdgcn_sched_barrier(0);
+    ANNETY_PRIO_LO();
     if (q + 1 < nsteps) compute_step(B);
   }
 }
@@ -180,19 +184,23 @@ __global__ __launch_bounds__(BLK) void crc32_oneround_kernel(const uint8_t* __re
   // next task's loads behind a branch the waitcnt pass merges the two paths and waits vmcnt(0) before
   // every fold, which serialises the A/B double buffer.
   for (int t = 0; t < ntasks; t += 2) {
+    ANNETY_PRIO_HI();
     {
       const uint4* s = reinterpret_cast<const uint4*>(t + 1 < ntasks ? lp + pstep : lp);
 #pragma unroll
       for (int i = 0; i < 8; i++) B[i] = s[i];
     }
     __builtin_amdgcn_sched_barrier(0);
+    ANNETY_PRIO_LO();
     finish(absorb_line(sinit, A, k, lds));
+    ANNETY_PRIO_HI();
     {
       const uint4* s = reinterpret_cast<const uint4*>(t + 2 < ntasks ? lp + 2 * pstep : lp);
 #pragma unroll
       for (int i = 0; i < 8; i++) A[i] = s[i];
     }
     __builtin_amdgcn_sched_barrier(0);
+    ANNETY_PRIO_LO();
     if (t + 1 < ntasks) finish(absorb_line(sinit, B, k, lds));
     lp += 2 * pstep;
   }
