@@ -5,6 +5,7 @@
 #include "../annety_amd/csrc/crc32_frames.hip"
 #include "../annety_amd/csrc/crc32_capi.cpp"
 #include <cstdio>
+#include <string>
 
 #define CK(x) do { hipError_t e_ = (x); if (e_ != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e_), __LINE__); exit(1);} } while (0)
 #define RC(x) do { int r_ = (x); if (r_) { printf("%s -> %d\n", #x, r_); exit(3); } } while (0)
@@ -15,8 +16,40 @@ void lines(DeviceCtx&, const ArenaLaunch& a) {
   CK(launch_arena_lines_p<PROBE>(a, 0));
 }
 
-int main() {
+// `arena_mb place`: the product line pass with the arena and the S/SB scratch at different offsets in
+// their allocations (does the placement of the two streams in HBM move the pass time?)
+int place() {
+  const size_t bytes = 1ull << 30, slack = 64ull << 20;
+  char* d0; uint32_t* s0;
+  CK(hipMalloc(&d0, bytes + slack)); CK(hipMemset(d0, 0x3C, bytes + slack));
+  RC(annety_crc_init(0));
+  DeviceCtx* c = nullptr; RC(current_ctx(&c));
+  ArenaLaunch a{};
+  arena_fill(*c, d0, bytes, a);
+  const size_t words = arena_geom(a).words;
+  CK(hipMalloc(&s0, words * 4 + slack));
+  hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  const size_t doffs[] = {0, 8192, 1 << 20, 32ull << 20};
+  const size_t soffs[] = {0, 1024, 4096, 65536, 1 << 20, 16ull << 20};
+  for (size_t dof : doffs)
+    for (size_t sof : soffs) {
+      ArenaLaunch b{};
+      arena_fill(*c, d0 + dof, bytes, b);
+      b.scratch = s0 + sof / 4;
+      for (int w = 0; w < 100; w++) CK(launch_arena_lines(b, 0));
+      CK(hipDeviceSynchronize());
+      CK(hipEventRecord(e0));
+      for (int r = 0; r < 100; r++) CK(launch_arena_lines(b, 0));
+      CK(hipEventRecord(e1)); CK(hipEventSynchronize(e1)); CK(hipGetLastError());
+      float ms; CK(hipEventElapsedTime(&ms, e0, e1));
+      printf("arena +%-10zu scratch +%-10zu %.4f ms\n", dof, sof, ms / 100);
+    }
+  return 0;
+}
+
+int main(int argc, char** argv) {
   setvbuf(stdout, nullptr, _IOLBF, 0);
+  if (argc > 1 && std::string(argv[1]) == "place") return place();
   const size_t bytes = 1ull << 30;
   char* d; uint32_t *scratch, *out;
   CK(hipMalloc(&d, bytes)); CK(hipMemset(d, 0x3C, bytes));
