@@ -58,17 +58,62 @@ __device__ __forceinline__ uint32_t nibble_map_set(uint32_t s, const uint32_t* l
   for (int k = 0; k < 8; k++) r[k] = t[k * T * 16 + __builtin_amdgcn_ubfe(s, 4 * k, 4)];
   return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6] ^ r[7]);
 }
+// ADJ: where the image starts in the full stitch layout (0, or kLdsHalfOff for the lite image, which
+// drops the slicing tables: see crc32_arena_stitch_lite_kernel).
 // shift_{-m} for m in [0, 128): U_hi[m >> 4] o U_lo[m & 15]
+template <uint32_t ADJ = 0>
 __device__ __forceinline__ uint32_t unshift(uint32_t t, uint32_t m, const uint32_t* lds) {
-  t = nibble_map_set<16>(t, lds, kLdsStitchUnshiftOff, m & 15u);
-  return nibble_map_set<8>(t, lds, kLdsStitchUnshiftOff + 8192, m >> 4);
+  t = nibble_map_set<16>(t, lds, kLdsStitchUnshiftOff - ADJ, m & 15u);
+  return nibble_map_set<8>(t, lds, kLdsStitchUnshiftOff + 8192 - ADJ, m >> 4);
 }
+template <uint32_t ADJ = 0>
 __device__ __forceinline__ uint32_t seg_map(uint32_t t, uint32_t idx, const uint32_t* lds) {
-  return nibble_map_set<32>(t, lds, kLdsMapOff, idx);
+  return nibble_map_set<32>(t, lds, kLdsMapOff - ADJ, idx);
 }
 
 __device__ __forceinline__ uint32_t gload4(uint64_t addr) {
   return *(const __attribute__((address_space(1))) uint32_t*)addr;
+}
+
+// Lite image (crc32_arena_stitch_lite_kernel): the window folds use a uniform nibble map shift_4 (8
+// conflict-free LDS reads per word) instead of the 128 KiB slicing tables. x = register ^ word becomes the
+// register after the word, pre-xored with the next one. Four 32-byte chains, as below.
+__device__ __forceinline__ void absorb_two_windows_lite(const uint4 (&v)[4], const uint4 (&w)[4], const uint32_t* lds,
+                                                        uint32_t off_word, uint32_t off_quarter, uint32_t& rv,
+                                                        uint32_t& rw) {
+  uint32_t xa = v[0].x, xb = v[2].x, xc = w[0].x, xd = w[2].x;
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    const uint32_t na[4] = {v[i].y, v[i].z, v[i].w, i == 0 ? v[1].x : 0u};
+    const uint32_t nb[4] = {v[2 + i].y, v[2 + i].z, v[2 + i].w, i == 0 ? v[3].x : 0u};
+    const uint32_t nc[4] = {w[i].y, w[i].z, w[i].w, i == 0 ? w[1].x : 0u};
+    const uint32_t nd[4] = {w[2 + i].y, w[2 + i].z, w[2 + i].w, i == 0 ? w[3].x : 0u};
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      xa = nibble_map_uniform(xa, lds, off_word) ^ na[q];
+      xb = nibble_map_uniform(xb, lds, off_word) ^ nb[q];
+      xc = nibble_map_uniform(xc, lds, off_word) ^ nc[q];
+      xd = nibble_map_uniform(xd, lds, off_word) ^ nd[q];
+    }
+  }
+  rv = nibble_map_uniform(xa, lds, off_quarter) ^ xb;
+  rw = nibble_map_uniform(xc, lds, off_quarter) ^ xd;
+}
+// One 128-byte line from register 0 with the lite image: two 64-byte chains joined by shift_64.
+__device__ __forceinline__ uint32_t absorb_line_lite(const uint4 (&u)[8], const uint32_t* lds, uint32_t off_word,
+                                                     uint32_t off_half) {
+  uint32_t xa = u[0].x, xb = u[4].x;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const uint32_t na[4] = {u[i].y, u[i].z, u[i].w, i < 3 ? u[i + 1].x : 0u};
+    const uint32_t nb[4] = {u[4 + i].y, u[4 + i].z, u[4 + i].w, i < 3 ? u[5 + i].x : 0u};
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      xa = nibble_map_uniform(xa, lds, off_word) ^ na[q];
+      xb = nibble_map_uniform(xb, lds, off_word) ^ nb[q];
+    }
+  }
+  return nibble_map_uniform(xa, lds, off_half) ^ xb;
 }
 
 // Two 64-byte windows from register 0, four 32-byte chains: raw(window) = shift_32(raw(first half)) ^
@@ -125,8 +170,9 @@ struct Vals {
 // B the S/SB words.
 //   PROBE (microbench only; product = 0): 1 = descriptors and stores only, 2 = + all loads,
 //   3 = + window folds (no map steps) - wrong digests, used to measure what the stages cost.
-template <bool UPD, int PROBE>
+template <bool UPD, int PROBE, bool LITE = false>
 struct Stitcher {
+  static constexpr uint32_t ADJ = LITE ? kLdsHalfOff : 0u;
   const StitchGeo& g;
   const uint32_t* lds;
   LaneCtx k;
@@ -260,18 +306,21 @@ struct Stitcher {
       mask_line<4>(v.h, (int32_t)y.hlo * 8, (int32_t)y.hhi * 8);
       mask_line<4>(v.t, (int32_t)y.tlo * 8, (int32_t)y.thi * 8);
       uint32_t wh, wt;
-      absorb_two_windows(v.h, v.t, k, lds, wh, wt);
+      if constexpr (LITE)
+        absorb_two_windows_lite(v.h, v.t, lds, kLdsWordOff - ADJ, kLdsQuarterOff - ADJ, wh, wt);
+      else
+        absorb_two_windows(v.h, v.t, k, lds, wh, wt);
       // head: V(first line start) = shift_{-lead}(s0) ^ shift_{-64}(wh), or
       //       V(first line end) = shift_{-lead}(shift_128(s0)) ^ wh
-      const uint32_t f1s = seg_map(v.s0, kMapF, lds);
-      const uint32_t u64 = nibble_map_set<8>(wh, lds, kLdsStitchUnshiftOff + 8192, 4);  // shift_{-64}
-      acc = unshift(y.headX ? v.s0 : f1s, y.lead, lds) ^ (y.headX ? u64 : wh);
+      const uint32_t f1s = seg_map<ADJ>(v.s0, kMapF, lds);
+      const uint32_t u64 = nibble_map_set<8>(wh, lds, kLdsStitchUnshiftOff + 8192 - ADJ, 4);  // shift_{-64}
+      acc = unshift<ADJ>(y.headX ? v.s0 : f1s, y.lead, lds) ^ (y.headX ? u64 : wh);
       if constexpr (PROBE != 3) {
 #pragma unroll
         for (int q = 0; q < 2; q++) {
           if ((y.act >> q) & 1u) {
             const uint32_t d = v.x[q] ^ (((y.yzero >> q) & 1u) ? 0u : v.y[q]);
-            acc = seg_map(acc, y.m1[q], lds) ^ seg_map(d, y.m2[q], lds);
+            acc = seg_map<ADJ>(acc, y.m1[q], lds) ^ seg_map<ADJ>(d, y.m2[q], lds);
           }
         }
         // whole superblocks between the partial ones: acc = shift_8KiB(acc) ^ SB[s,0]
@@ -282,33 +331,38 @@ struct Stitcher {
           }
 #pragma unroll
           for (int q = 0; q < 8; q++)
-            if (i + q < y.nmid) acc = seg_map(acc, kMapG + 7, lds) ^ v.mid[q];
+            if (i + q < y.nmid) acc = seg_map<ADJ>(acc, kMapG + 7, lds) ^ v.mid[q];
         }
 #pragma unroll
         for (int q = 2; q < 4; q++) {
           if ((y.act >> q) & 1u) {
             const uint32_t d = v.x[q] ^ (((y.yzero >> q) & 1u) ? 0u : v.y[q]);
-            acc = seg_map(acc, y.m1[q], lds) ^ seg_map(d, y.m2[q], lds);
+            acc = seg_map<ADJ>(acc, y.m1[q], lds) ^ seg_map<ADJ>(d, y.m2[q], lds);
           }
         }
       }
       // tail: V(E) = shift_{-(128-te)}(V(last line end) ^ wt), or
       //       shift_{-(128-te)}(shift_128(V(last line start)) ^ shift_64(wt))
-      const uint32_t f1a = seg_map(acc, kMapF, lds);
-      const uint32_t h64 = nibble_map_uniform(wt, lds, kLdsHalfOff);
-      acc = unshift(y.tailX ? acc ^ wt : f1a ^ h64, 128 - y.te, lds);
+      const uint32_t f1a = seg_map<ADJ>(acc, kMapF, lds);
+      const uint32_t h64 = nibble_map_uniform(wt, lds, kLdsHalfOff - ADJ);
+      acc = unshift<ADJ>(y.tailX ? acc ^ wt : f1a ^ h64, 128 - y.te, lds);
     } else {
       // payload reaches outside the arena the caller declared (or there is none): fold its lines directly
       const uint64_t L0 = y.A >> 7, L1 = (y.E - 1) >> 7;
-      acc = unshift(v.s0, y.lead, lds);  // V(first line start): the lead bytes are zeros here
+      acc = unshift<ADJ>(v.s0, y.lead, lds);  // V(first line start): the lead bytes are zeros here
       for (uint64_t i = L0; i <= L1; i++) {
         uint4 u[8];
 #pragma unroll
         for (int q = 0; q < 8; q++) u[q] = gload16((i << 7) + 16 * q);
         mask_line<8>(u, i == L0 ? (int32_t)y.lead * 8 : 0, i == L1 ? (int32_t)y.te * 8 : 1024);
-        acc = seg_map(acc, kMapF, lds) ^ absorb_line(0u, u, k, lds);
+        uint32_t r;
+        if constexpr (LITE)
+          r = absorb_line_lite(u, lds, kLdsWordOff - ADJ, kLdsHalfOff - ADJ);
+        else
+          r = absorb_line(0u, u, k, lds);
+        acc = seg_map<ADJ>(acc, kMapF, lds) ^ r;
       }
-      acc = unshift(acc, 128 - y.te, lds);  // drop the zero bytes after the payload end
+      acc = unshift<ADJ>(acc, 128 - y.te, lds);  // drop the zero bytes after the payload end
     }
     g.out[p] = UPD ? acc : ~acc;
   }
@@ -399,6 +453,33 @@ __global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchGeo g, co
   }
 }
 
+// Lite stitch (microbench A/B): the image without the slicing tables (30 KiB instead of 157 KiB), so
+// several blocks fit a CU; one payload per lane, WPE = minimum waves per SIMD the compiler must allow.
+template <bool UPD, int BLK, int WPE>
+__global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(WPE))) void crc32_arena_stitch_lite_kernel(
+    StitchGeo g, const uint4* __restrict__ img_lite) {
+  __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsLiteBytes / 16];
+  const Stitcher<UPD, 0, true> st{g, reinterpret_cast<const uint32_t*>(lds4), lane_ctx()};
+  const size_t per = (g.n + gridDim.x - 1) / gridDim.x;
+  const size_t p_end = std::min(g.n, (size_t)(blockIdx.x + 1) * per);
+  const size_t p_first = (size_t)blockIdx.x * per + threadIdx.x;
+  Plan y{};
+  Vals v{};
+  if (p_first < p_end) {
+    st.plan_a(p_first, y, v);
+    st.plan_b(p_first, y, v);
+  }
+  load_image<kLdsLiteBytes, BLK>(lds4, img_lite, nullptr);
+  __syncthreads();
+  for (size_t p = p_first; p < p_end; p += BLK) {
+    if (p != p_first) {
+      st.plan_a(p, y, v);
+      st.plan_b(p, y, v);
+    }
+    st.process(p, y, v);
+  }
+}
+
 // First launch: the line pass.
 template <int PROBE = 0>
 __global__ __launch_bounds__(kBlock) void crc32_arena_lines_kernel(const uint8_t* __restrict__ base, LineOut ar,
@@ -470,6 +551,19 @@ hipError_t launch_stitch_p(const ArenaLaunch& a, hipStream_t stream) {
   else
     hipLaunchKernelGGL((crc32_arena_stitch_kernel<false, kStitchBlock, PROBE, PIPE>), dim3((unsigned)blocks),
                        dim3(kStitchBlock), 0, stream, s, img_slice, img_stitch);
+  return hipGetLastError();
+}
+
+// blocks: 0 = one payload per lane (ceil(n / BLK))
+template <int BLK, int WPE>
+hipError_t launch_stitch_lite(const ArenaLaunch& a, const void* img_lite, size_t blocks, hipStream_t stream) {
+  const StitchGeo s = stitch_geo(a, arena_geom(a));
+  if (!blocks) blocks = std::max<size_t>(1, (a.n + BLK - 1) / BLK);
+  const uint4* img = static_cast<const uint4*>(img_lite);
+  if (a.update)
+    hipLaunchKernelGGL((crc32_arena_stitch_lite_kernel<true, BLK, WPE>), dim3((unsigned)blocks), dim3(BLK), 0, stream, s, img);
+  else
+    hipLaunchKernelGGL((crc32_arena_stitch_lite_kernel<false, BLK, WPE>), dim3((unsigned)blocks), dim3(BLK), 0, stream, s, img);
   return hipGetLastError();
 }
 

@@ -128,5 +128,9 @@ constexpr uint32_t kMapF = 0, kMapG = 8, kMapUL = 16, kMapUB = 24;  // map index
 constexpr uint32_t kLdsStitchUnshiftOff = kLdsMapOff + kLdsMapBytes;
 constexpr uint32_t kLdsQuarterOff = kLdsStitchUnshiftOff + kLdsUnshiftBytes;
 constexpr uint32_t kLdsStitchImageBytes = kLdsQuarterOff + 512;  // 160768 <= 163840
+// Lite stitch image (crc32_arena_stitch_lite_kernel): [kLdsHalfOff, kLdsStitchImageBytes) of the stitch
+// layout (half-line join, segment maps, inverse shifts, quarter join) + shift_4 nibble map, 30 KiB.
+constexpr uint32_t kLdsWordOff = kLdsStitchImageBytes;  // in the stitch layout's coordinates
+constexpr uint32_t kLdsLiteBytes = kLdsWordOff + 512 - kLdsHalfOff;  // 30208
 
 }  // namespace annety_crc
