@@ -78,7 +78,7 @@ __device__ __forceinline__ uint32_t gload4(uint64_t addr) {
 // Lite image (crc32_arena_stitch_lite_kernel): the window folds use a uniform nibble map shift_4 (8
 // conflict-free LDS reads per word) instead of the 128 KiB slicing tables. x = register ^ word becomes the
 // register after the word, pre-xored with the next one. Four 32-byte chains, as below.
-__device__ __forceinline__ void absorb_two_windows_lite(const uint4 (&v)[4], const uint4 (&w)[4], const uint32_t* lds,
+[[maybe_unused]] __device__ __forceinline__ void absorb_two_windows_lite(const uint4 (&v)[4], const uint4 (&w)[4], const uint32_t* lds,
                                                         uint32_t off_word, uint32_t off_quarter, uint32_t& rv,
                                                         uint32_t& rw) {
   uint32_t xa = v[0].x, xb = v[2].x, xc = w[0].x, xd = w[2].x;
@@ -100,7 +100,7 @@ __device__ __forceinline__ void absorb_two_windows_lite(const uint4 (&v)[4], con
   rw = nibble_map_uniform(xc, lds, off_quarter) ^ xd;
 }
 // One 128-byte line from register 0 with the lite image: two 64-byte chains joined by shift_64.
-__device__ __forceinline__ uint32_t absorb_line_lite(const uint4 (&u)[8], const uint32_t* lds, uint32_t off_word,
+[[maybe_unused]] __device__ __forceinline__ uint32_t absorb_line_lite(const uint4 (&u)[8], const uint32_t* lds, uint32_t off_word,
                                                      uint32_t off_half) {
   uint32_t xa = u[0].x, xb = u[4].x;
 #pragma unroll
