@@ -320,17 +320,18 @@ struct DeviceCtx {
   std::mutex stg_mu;  // one host-staged batch at a time per device
   std::mutex pow_mu;  // split-path power tables, one per segment size
   std::vector<std::pair<uint64_t, uint32_t*>> powers;
-  // arena-path scratch, reused across calls (run_arena): each slot's last use is fenced by an event that
-  // a later call on any stream waits for, so reuse is safe whatever streams the callers use
+  // arena-path scratch, reused across calls (run_arena): one slot per stream, fenced by stream order
   struct ScratchSlot {
     void* ptr = nullptr;
     size_t bytes = 0;
     hipStream_t last = nullptr;
-    hipEvent_t done = nullptr;
+    bool used = false;
+    hipEvent_t done = nullptr;  // ANNETY_CRC_ARENA_EVENTS=1 only: the last use, recorded per call
   };
   std::mutex arena_mu;  // held while a call picks a slot and enqueues its two launches
   ScratchSlot arena_slot[8];
   int arena_slots = 0;
+  unsigned arena_evict = 0;
 };
 
 constexpr int kMaxDev = 64;
@@ -512,23 +513,36 @@ int run_arena(DeviceCtx& c, const void* d_base, size_t arena_bytes, const uint64
     const hipError_t e = launch_arena(a, stream);
     return e == hipSuccess ? ANNETY_CRC_OK : hip_fail(e);
   }
-  // scratch slot: the one this stream used last, else one whose last use has finished, else a new one,
-  // else slot 0 behind its event (the stream-ordered allocator cost ~3.6 us per call)
+  // Scratch slot: the one this stream used last (stream order fences it), else a new one (up to 8), else
+  // one taken over from another stream after hipDeviceSynchronize (a ninth concurrent stream; rare).
+  // No per-call event: recording one after each call cost ~2 us of GPU time per call (a marker between
+  // this call's stitch and the next call's line pass: product call 215.3 us vs the two launches alone
+  // 213.1, profiles/r02/session5/stitch_mb.log). ANNETY_CRC_ARENA_EVENTS=1 restores the per-call event
+  // fence (any slot whose last use has finished can serve any stream), for A/B runs. (The
+  // stream-ordered allocator cost ~3.6 us per call.)
+  static const bool events = [] {
+    const char* e = std::getenv("ANNETY_CRC_ARENA_EVENTS");
+    return e && e[0] == '1';
+  }();
   const size_t bytes = arena_geom(a).words * sizeof(uint32_t);
   std::lock_guard<std::mutex> lk(c.arena_mu);
   DeviceCtx::ScratchSlot* slot = nullptr;
   for (int i = 0; i < c.arena_slots && !slot; i++)
-    if (c.arena_slot[i].last == stream) slot = &c.arena_slot[i];
-  for (int i = 0; i < c.arena_slots && !slot; i++)
-    if (hipEventQuery(c.arena_slot[i].done) == hipSuccess) slot = &c.arena_slot[i];
+    if (c.arena_slot[i].used && c.arena_slot[i].last == stream) slot = &c.arena_slot[i];
+  if (events)
+    for (int i = 0; i < c.arena_slots && !slot; i++)
+      if (hipEventQuery(c.arena_slot[i].done) == hipSuccess) slot = &c.arena_slot[i];
   if (!slot && c.arena_slots < 8) {
     DeviceCtx::ScratchSlot& fresh = c.arena_slot[c.arena_slots];
     HIP_TRY(hipEventCreateWithFlags(&fresh.done, hipEventDisableTiming));
     c.arena_slots++;
     slot = &fresh;
   }
-  if (!slot) slot = &c.arena_slot[0];
-  if (slot->last && slot->last != stream) HIP_TRY(hipStreamWaitEvent(stream, slot->done, 0));
+  if (!slot) {
+    slot = &c.arena_slot[c.arena_evict++ % 8];
+    if (!events) HIP_TRY(hipDeviceSynchronize());  // every earlier use of the slot has finished
+  }
+  if (events && slot->used && slot->last != stream) HIP_TRY(hipStreamWaitEvent(stream, slot->done, 0));
   if (slot->bytes < bytes) {
     if (slot->ptr) HIP_TRY(hipFreeAsync(slot->ptr, stream));
     slot->ptr = nullptr;
@@ -538,8 +552,9 @@ int run_arena(DeviceCtx& c, const void* d_base, size_t arena_bytes, const uint64
   }
   a.scratch = static_cast<uint32_t*>(slot->ptr);
   const hipError_t e = launch_arena(a, stream);
-  const hipError_t r = hipEventRecord(slot->done, stream);
+  const hipError_t r = events ? hipEventRecord(slot->done, stream) : hipSuccess;
   slot->last = stream;
+  slot->used = true;
   if (e != hipSuccess) return hip_fail(e);
   return r == hipSuccess ? ANNETY_CRC_OK : hip_fail(r);
 }
@@ -701,6 +716,7 @@ int annety_crc_shutdown(void) {
     }
     {
       std::lock_guard<std::mutex> al(c.arena_mu);
+      if (c.arena_slots) (void)hipDeviceSynchronize();  // slots carry no event per call: drain their last uses
       for (int i = 0; i < c.arena_slots; i++) {
         DeviceCtx::ScratchSlot& sl = c.arena_slot[i];
         (void)hipEventSynchronize(sl.done);
