@@ -320,7 +320,8 @@ struct DeviceCtx {
   std::mutex stg_mu;  // one host-staged batch at a time per device
   std::mutex pow_mu;  // split-path power tables, one per segment size
   std::vector<std::pair<uint64_t, uint32_t*>> powers;
-  // arena-path scratch, reused across calls (run_arena): one slot per stream, fenced by stream order
+  // per-call scratch of the arena, split and sorted paths, reused across calls: one slot per stream,
+  // fenced by stream order (scratch_slot)
   struct ScratchSlot {
     void* ptr = nullptr;
     size_t bytes = 0;
@@ -453,26 +454,82 @@ int run_var(DeviceCtx& c, const void* d_base, size_t n, uint64_t fstride, uint32
   return ANNETY_CRC_OK;
 }
 
+// Per-call device scratch of the arena, split and sorted paths: the slot this stream used last (stream
+// order fences it), else a new one (up to 8), else one taken over from another stream after
+// hipDeviceSynchronize (a ninth concurrent stream; rare). The caller holds c.arena_mu from here until its
+// launches are enqueued, then calls scratch_done. No per-call event: recording one after each call cost
+// 2-4 us of GPU time per call (a marker between one call's last kernel and the next call's first; config 3
+// 0.2111-0.2173 vs 0.2068-0.2089 ms per step, profiles/r02/arena_events_ab/). ANNETY_CRC_ARENA_EVENTS=1
+// restores the per-call event fence (any slot whose last use has finished can serve any stream), for A/B
+// runs. The stream-ordered allocator (hipMallocAsync/hipFreeAsync per call) cost ~3.6 us per call.
+bool scratch_events() {
+  static const bool events = [] {
+    const char* e = std::getenv("ANNETY_CRC_ARENA_EVENTS");
+    return e && e[0] == '1';
+  }();
+  return events;
+}
+
+int scratch_slot(DeviceCtx& c, hipStream_t stream, size_t bytes, DeviceCtx::ScratchSlot** out) {
+  const bool events = scratch_events();
+  DeviceCtx::ScratchSlot* slot = nullptr;
+  for (int i = 0; i < c.arena_slots && !slot; i++)
+    if (c.arena_slot[i].used && c.arena_slot[i].last == stream) slot = &c.arena_slot[i];
+  if (events)
+    for (int i = 0; i < c.arena_slots && !slot; i++)
+      if (hipEventQuery(c.arena_slot[i].done) == hipSuccess) slot = &c.arena_slot[i];
+  if (!slot && c.arena_slots < 8) {
+    DeviceCtx::ScratchSlot& fresh = c.arena_slot[c.arena_slots];
+    HIP_TRY(hipEventCreateWithFlags(&fresh.done, hipEventDisableTiming));
+    c.arena_slots++;
+    slot = &fresh;
+  }
+  if (!slot) {
+    slot = &c.arena_slot[c.arena_evict++ % 8];
+    if (!events) HIP_TRY(hipDeviceSynchronize());  // every earlier use of the slot has finished
+  }
+  if (events && slot->used && slot->last != stream) HIP_TRY(hipStreamWaitEvent(stream, slot->done, 0));
+  if (slot->bytes < bytes) {
+    if (slot->ptr) HIP_TRY(hipFreeAsync(slot->ptr, stream));
+    slot->ptr = nullptr;
+    slot->bytes = 0;
+    HIP_TRY(hipMallocAsync(&slot->ptr, bytes, stream));
+    slot->bytes = bytes;
+  }
+  *out = slot;
+  return ANNETY_CRC_OK;
+}
+
+// After the call's launches on `stream` (arena_mu still held): the slot's last user.
+int scratch_done(DeviceCtx::ScratchSlot* slot, hipStream_t stream) {
+  slot->last = stream;
+  slot->used = true;
+  if (!scratch_events()) return ANNETY_CRC_OK;
+  const hipError_t r = hipEventRecord(slot->done, stream);
+  return r == hipSuccess ? ANNETY_CRC_OK : hip_fail(r);
+}
+
 // Variable batch: bucket by line count on the device (no host round trip), then one launch per
-// length class with its own lane-group width. Scratch comes from the stream-ordered allocator.
+// length class with its own lane-group width. Scratch: the stream's slot (scratch_slot).
 int run_var_sorted(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_off, const uint32_t* d_len,
                    uint32_t* d_out, hipStream_t stream, bool update = false) {
   const size_t rows_words = (size_t)bucket_blocks(n) * bucket_count();
   const size_t head = (rows_words + 8) * sizeof(uint32_t);  // rows + ranges (16-byte multiple)
-  char* scratch = nullptr;
-  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&scratch), head + 16 * n, stream));
+  std::lock_guard<std::mutex> lk(c.arena_mu);
+  DeviceCtx::ScratchSlot* slot = nullptr;
+  int rc = scratch_slot(c, stream, head + 16 * n, &slot);
+  if (rc) return rc;
+  char* scratch = static_cast<char*>(slot->ptr);
   uint32_t* rows = reinterpret_cast<uint32_t*>(scratch);
   uint32_t* ranges = rows + rows_words;
   void* desc = scratch + head;
-  int rc = ANNETY_CRC_OK;
   hipError_t e = launch_bucket(d_base, n, d_off, d_len, rows, ranges, desc, update ? nullptr : d_out, stream);
   if (e != hipSuccess) rc = hip_fail(e);
   const uint32_t groups[3] = {32, 16, 4};  // lanes per payload of the long / middle / small class
   for (int k = 0; k < 3 && rc == ANNETY_CRC_OK; k++)
     rc = run_var(c, d_base, n, 0, 0, groups[k], desc, ranges + 2 * k, d_out, stream, update);
-  e = hipFreeAsync(scratch, stream);
-  if (rc == ANNETY_CRC_OK && e != hipSuccess) rc = hip_fail(e);
-  return rc;
+  const int rd = scratch_done(slot, stream);
+  return rc ? rc : rd;
 }
 
 // Arena path (crc32_arena.hip): one bulk pass over every line of [d_base, d_base + arena_bytes),
@@ -513,50 +570,16 @@ int run_arena(DeviceCtx& c, const void* d_base, size_t arena_bytes, const uint64
     const hipError_t e = launch_arena(a, stream);
     return e == hipSuccess ? ANNETY_CRC_OK : hip_fail(e);
   }
-  // Scratch slot: the one this stream used last (stream order fences it), else a new one (up to 8), else
-  // one taken over from another stream after hipDeviceSynchronize (a ninth concurrent stream; rare).
-  // No per-call event: recording one after each call cost ~2 us of GPU time per call (a marker between
-  // this call's stitch and the next call's line pass: product call 215.3 us vs the two launches alone
-  // 213.1, profiles/r02/session5/stitch_mb.log). ANNETY_CRC_ARENA_EVENTS=1 restores the per-call event
-  // fence (any slot whose last use has finished can serve any stream), for A/B runs. (The
-  // stream-ordered allocator cost ~3.6 us per call.)
-  static const bool events = [] {
-    const char* e = std::getenv("ANNETY_CRC_ARENA_EVENTS");
-    return e && e[0] == '1';
-  }();
   const size_t bytes = arena_geom(a).words * sizeof(uint32_t);
   std::lock_guard<std::mutex> lk(c.arena_mu);
   DeviceCtx::ScratchSlot* slot = nullptr;
-  for (int i = 0; i < c.arena_slots && !slot; i++)
-    if (c.arena_slot[i].used && c.arena_slot[i].last == stream) slot = &c.arena_slot[i];
-  if (events)
-    for (int i = 0; i < c.arena_slots && !slot; i++)
-      if (hipEventQuery(c.arena_slot[i].done) == hipSuccess) slot = &c.arena_slot[i];
-  if (!slot && c.arena_slots < 8) {
-    DeviceCtx::ScratchSlot& fresh = c.arena_slot[c.arena_slots];
-    HIP_TRY(hipEventCreateWithFlags(&fresh.done, hipEventDisableTiming));
-    c.arena_slots++;
-    slot = &fresh;
-  }
-  if (!slot) {
-    slot = &c.arena_slot[c.arena_evict++ % 8];
-    if (!events) HIP_TRY(hipDeviceSynchronize());  // every earlier use of the slot has finished
-  }
-  if (events && slot->used && slot->last != stream) HIP_TRY(hipStreamWaitEvent(stream, slot->done, 0));
-  if (slot->bytes < bytes) {
-    if (slot->ptr) HIP_TRY(hipFreeAsync(slot->ptr, stream));
-    slot->ptr = nullptr;
-    slot->bytes = 0;
-    HIP_TRY(hipMallocAsync(&slot->ptr, bytes, stream));
-    slot->bytes = bytes;
-  }
+  const int rc = scratch_slot(c, stream, bytes, &slot);
+  if (rc) return rc;
   a.scratch = static_cast<uint32_t*>(slot->ptr);
   const hipError_t e = launch_arena(a, stream);
-  const hipError_t r = events ? hipEventRecord(slot->done, stream) : hipSuccess;
-  slot->last = stream;
-  slot->used = true;
+  const int rd = scratch_done(slot, stream);
   if (e != hipSuccess) return hip_fail(e);
-  return r == hipSuccess ? ANNETY_CRC_OK : hip_fail(r);
+  return rd;
 }
 
 bool fixed_fast_ok(const void* d_base, size_t len, size_t stride) {
@@ -632,8 +655,10 @@ int run_split(DeviceCtx& c, const void* d_base, size_t n, uint64_t len, uint64_t
   int rc = split_powers(c, seg, &powers);
   if (rc) return rc;
   const size_t crc_bytes = (tasks * 4 + 15) & ~(size_t)15;
-  char* scratch = nullptr;
-  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&scratch), 16 + crc_bytes + 16 * tasks, stream));
+  std::lock_guard<std::mutex> lk(c.arena_mu);
+  DeviceCtx::ScratchSlot* slot = nullptr;
+  if ((rc = scratch_slot(c, stream, 16 + crc_bytes + 16 * tasks, &slot))) return rc;
+  char* scratch = static_cast<char*>(slot->ptr);
   uint32_t* range = reinterpret_cast<uint32_t*>(scratch);
   uint32_t* seg_crc = reinterpret_cast<uint32_t*>(scratch + 16);
   void* desc = scratch + 16 + crc_bytes;
@@ -648,9 +673,8 @@ int run_split(DeviceCtx& c, const void* d_base, size_t n, uint64_t len, uint64_t
     hipError_t e = launch_split_join(seg_crc, n, S, powers, d_out, stream);
     if (e != hipSuccess) rc = hip_fail(e);
   }
-  hipError_t e = hipFreeAsync(scratch, stream);
-  if (rc == ANNETY_CRC_OK && e != hipSuccess) rc = hip_fail(e);
-  return rc;
+  const int rd = scratch_done(slot, stream);
+  return rc ? rc : rd;
 }
 
 }  // namespace
