@@ -13,6 +13,10 @@
  * Error model (the reference functions are total): every entry point that can fail
  * returns an int status, 0 on success, a negative ANNETY_CRC_E* code otherwise, and never aborts.
  * Thread safety: all entry points are reentrant; device state is initialised once per device.
+ * Streams: the variable, arena and split paths keep per-call device scratch per (device, stream), reused
+ * in stream order. Up to 8 streams per device hold their own; a further stream takes one over after a
+ * device-wide synchronise. Do not destroy a stream while a call on it is still running and then pass a
+ * new stream that reuses its handle: that is a race, as it is with any stream-ordered resource.
  */
 #ifndef ANNETY_CRC_H
 #define ANNETY_CRC_H
