@@ -22,6 +22,11 @@ struct LineOut {
 // `base` = the first full superblock (fs0 * 8192), passed as its own kernel argument: loads through a
 // __restrict__ kernel-argument pointer compile to the config-1 kernel's schedule; the same loads through
 // integer-built address-space-1 pointers ran this pass 30 % slower (microbench/arena_mb.hip).
+// S bursts: nontemporal stores (1, the product) or default-policy stores (0, microbench A/B: they would
+// leave S in the caches for the stitch).
+#ifndef ANNETY_S_NT
+#define ANNETY_S_NT 1
+#endif
 template <int PROBE = 0>
 __device__ __forceinline__ void arena_line_pass(const uint8_t* __restrict__ base, const LineOut& ar, uint32_t bid,
                                                 uint32_t nbid, uint4* lds4,
@@ -121,8 +126,13 @@ __device__ __forceinline__ void arena_line_pass(const uint8_t* __restrict__ base
       if constexpr ((PROBE & 1) == 0) {
         const v4u32 lo = {q[0], q[1], q[2], q[3]}, hi = {q[4], q[5], q[6], q[7]};
         v4u32* dst = reinterpret_cast<v4u32*>(ar.S + arena_s_word(t0, gid, j, ar.W));
-        __builtin_nontemporal_store(lo, dst);
-        __builtin_nontemporal_store(hi, dst + 64);  // + 1 KiB
+        if constexpr (ANNETY_S_NT) {
+          __builtin_nontemporal_store(lo, dst);
+          __builtin_nontemporal_store(hi, dst + 64);  // + 1 KiB
+        } else {
+          dst[0] = lo;
+          dst[64] = hi;
+        }
       }
     }
   };
