@@ -31,6 +31,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "crc32_arena_lines.h"
 #include "crc32_device.h"
@@ -584,7 +585,14 @@ hipError_t launch_arena(const ArenaLaunch& a, hipStream_t stream) {
     const hipError_t e = launch_arena_lines(a, stream);
     if (e != hipSuccess) return e;
   }
-  return launch_stitch_p<0>(a, stream);
+  // The stitch issues a lane's next payload loads before folding the current one (PIPE 1): config-3 step
+  // 0.2139-0.2142 ms vs 0.2144-0.2151 without, same box, three alternating pairs
+  // (profiles/r02/stitch_pipe_bench_ab/). ANNETY_CRC_STITCH_PIPE=0 selects the one-payload-at-a-time loop.
+  static const bool pipe = [] {
+    const char* e = std::getenv("ANNETY_CRC_STITCH_PIPE");
+    return !(e && e[0] == '0');
+  }();
+  return pipe ? launch_stitch_p<0, 1>(a, stream) : launch_stitch_p<0>(a, stream);
 }
 
 }  // namespace annety_crc
