@@ -26,6 +26,9 @@ from .crc32c import (  # noqa: F401
     StreamingCrc,
     digests_to_numpy,
     reserve_cus,
+    scratch_stats,
+    set_split,
+    stream_release,
     tables,
 )
 from ._lib import CrcError, lib_path  # noqa: F401
@@ -43,6 +46,9 @@ __all__ = [
     "crc32_combine",
     "digests_to_numpy",
     "reserve_cus",
+    "scratch_stats",
+    "set_split",
+    "stream_release",
     "tables",
     "LengthHeaderCodec",
     "ProtobufCodecFrames",

@@ -22,6 +22,10 @@ SIGNATURES = [
     ("annety_crc_strerror", ctypes.c_char_p, [ctypes.c_int]),
     ("annety_crc_last_hip_error", ctypes.c_int, []),
     ("annety_crc_reserve_cus", ctypes.c_int, [ctypes.c_int]),
+    ("annety_crc_set_split", ctypes.c_int, [ctypes.c_int, _u64]),
+    ("annety_crc_stream_release", ctypes.c_int, [_vp]),
+    ("annety_crc_scratch_stats", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_u64), ctypes.POINTER(_u64),
+                                                ctypes.POINTER(_u64)]),
     ("annety_crc32_long", _u32, [_vp, _c_size]),
     ("annety_crc32_short", _u32, [_vp, _c_size]),
     ("annety_crc32_update", None, [ctypes.POINTER(_u32), _vp, _c_size]),
@@ -38,6 +42,7 @@ SIGNATURES = [
     ("annety_crc_host_register", ctypes.c_int, [_vp, _c_size]),
     ("annety_crc_host_unregister", ctypes.c_int, [_vp]),
     ("annety_crc_shard_plan", ctypes.c_int, [_c_size, ctypes.c_int, _vp, _vp]),
+    ("annety_crc_group_schedule", ctypes.c_int, [_vp, ctypes.c_int, _c_size, _vp]),
     ("annety_crc_group_create", ctypes.c_int, [_vp, ctypes.c_int, ctypes.POINTER(_vp)]),
     ("annety_crc_group_destroy", ctypes.c_int, [_vp]),
     ("annety_crc_group_size", ctypes.c_int, [_vp]),

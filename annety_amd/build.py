@@ -5,6 +5,7 @@ Pure hipcc command lines (no torch extension machinery): the product is a plain 
 """
 from __future__ import annotations
 
+import concurrent.futures
 import os
 import shutil
 import subprocess
@@ -43,10 +44,10 @@ def up_to_date() -> bool:
 def build(force: bool = False, verbose: bool = False) -> str:
     if not force and up_to_date():
         return LIB
-    objs = []
     tmp = os.path.join(PKG, "build")
     os.makedirs(tmp, exist_ok=True)
     common = ["-std=c++17", "-O3", "-fPIC", f"-I{INCLUDE}", f"-I{CSRC}", "-Wall"]
+    cmds, objs = [], []
     for s in SOURCES:
         src = os.path.join(CSRC, s)
         obj = os.path.join(tmp, s + ".o")
@@ -55,8 +56,12 @@ def build(force: bool = False, verbose: bool = False) -> str:
             cmd[1:1] = [f"--offload-arch={ARCH}"]
         if verbose:
             print(" ".join(cmd))
-        subprocess.run(cmd, check=True)
+        cmds.append(cmd)
         objs.append(obj)
+    # the translation units are independent: compile them side by side
+    with concurrent.futures.ThreadPoolExecutor(max_workers=min(len(cmds), 8)) as ex:
+        for f in [ex.submit(subprocess.run, c, check=True) for c in cmds]:
+            f.result()
     out_tmp = LIB + ".tmp"
     # RCCL for the device-group entry points (crc32_group.cpp); rpath so the library loads without
     # LD_LIBRARY_PATH on any box with this ROCm image

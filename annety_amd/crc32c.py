@@ -81,6 +81,36 @@ def reserve_cus(n: int) -> None:
     _lib.check(_lib.get().annety_crc_reserve_cus(int(n)), "annety_crc_reserve_cus")
 
 
+def set_split(mode: int = -1, min_segment: int = 0) -> None:
+    """annety_crc_set_split: long-payload split policy (-1 auto, 0 never, 1 always), process-wide."""
+    _lib.check(_lib.get().annety_crc_set_split(int(mode), int(min_segment)), "annety_crc_set_split")
+
+
+def scratch_stats(device: int = 0) -> dict:
+    """annety_crc_scratch_stats: streams holding a scratch slot on `device`, slot hand-overs between
+    streams and device-wide synchronisations so far."""
+    import ctypes
+
+    v = [ctypes.c_uint64() for _ in range(3)]
+    _lib.check(_lib.get().annety_crc_scratch_stats(int(device), *[ctypes.byref(x) for x in v]),
+               "annety_crc_scratch_stats")
+    return {"slots": v[0].value, "handoffs": v[1].value, "device_syncs": v[2].value}
+
+
+def stream_release(stream) -> None:
+    """annety_crc_stream_release: drop a stream's scratch (stream-ordered) before the stream is destroyed."""
+    h = stream if isinstance(stream, int) else int(stream.cuda_stream)
+    dev = getattr(stream, "device", None)
+    with _on_device(stream) if dev is not None else _nullctx():
+        _lib.check(_lib.get().annety_crc_stream_release(h), "annety_crc_stream_release")
+
+
+def _nullctx():
+    import contextlib
+
+    return contextlib.nullcontext()
+
+
 def tables() -> tuple[np.ndarray, np.ndarray]:
     """The drop-in's annety::internal::crc32_table256/16 (src/Crc32c.cc:20-92)."""
     lib = _lib.get()

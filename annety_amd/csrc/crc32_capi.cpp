@@ -11,6 +11,7 @@
 #include <condition_variable>
 #include <cstring>
 #include <functional>
+#include <memory>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -325,14 +326,17 @@ struct DeviceCtx {
   struct ScratchSlot {
     void* ptr = nullptr;
     size_t bytes = 0;
-    hipStream_t last = nullptr;
-    bool used = false;
-    hipEvent_t done = nullptr;  // ANNETY_CRC_ARENA_EVENTS=1 only: the last use, recorded per call
+    hipStream_t last = nullptr;  // the stream of the last call that used the slot
+    std::thread::id tid{};       // last == hipStreamPerThread: the thread the handle resolved to
+    uint64_t tick = 0;           // last use, for LRU hand-over
+    hipEvent_t fence = nullptr;  // recorded on `last` only when the slot is handed to another stream
+                                 // (per-thread handles: after every call, see scratch_done)
   };
-  std::mutex arena_mu;  // held while a call picks a slot and enqueues its two launches
-  ScratchSlot arena_slot[8];
-  int arena_slots = 0;
-  unsigned arena_evict = 0;
+  std::mutex arena_mu;  // held while a call picks a slot and enqueues its launches
+  std::vector<std::unique_ptr<ScratchSlot>> slots;
+  uint64_t tick = 0;
+  // test-visible counters (annety_crc_scratch_stats)
+  std::atomic<uint64_t> handoffs{0}, device_syncs{0};
 };
 
 constexpr int kMaxDev = 64;
@@ -342,6 +346,15 @@ DeviceCtx g_dev[kMaxDev];
 std::atomic<int> g_reserved_cus{0};
 size_t grid_cus(const DeviceCtx& c) { return (size_t)std::max(1, c.cus - g_reserved_cus.load()); }
 std::mutex g_init_mu;
+
+void free_images(DeviceCtx& c) {
+  void* bufs[] = {c.d_slice, c.d_groups, c.d_unshift, c.d_short, c.d_sb, c.d_stitch, c.d_zero};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  c.d_slice = c.d_groups = nullptr;
+  c.d_unshift = c.d_short = nullptr;
+  c.d_sb = c.d_stitch = c.d_zero = nullptr;
+}
 
 int init_device_locked(int dev) {
   DeviceCtx& c = g_dev[dev];
@@ -376,21 +389,49 @@ int init_device_locked(int dev) {
     c.cus = prop.multiProcessorCount;
     c.ready = true;
   } while (0);
+  if (rc != ANNETY_CRC_OK) free_images(c);  // nothing half-built survives a failed init
   (void)hipSetDevice(prev);
   return rc;
 }
 
-int current_ctx(DeviceCtx** out) {
-  int dev = 0;
-  HIP_TRY(hipGetDevice(&dev));
-  if (dev < 0 || dev >= kMaxDev) return ANNETY_CRC_ENODEV;
+DeviceCtx* ensure_ctx(int dev, int* rc) {
+  if (dev < 0 || dev >= kMaxDev) {
+    *rc = ANNETY_CRC_ENODEV;
+    return nullptr;
+  }
   DeviceCtx& c = g_dev[dev];
   if (!c.ready) {
     std::lock_guard<std::mutex> lk(g_init_mu);
-    int rc = init_device_locked(dev);
-    if (rc != ANNETY_CRC_OK) return rc;
+    *rc = init_device_locked(dev);
+    if (*rc != ANNETY_CRC_OK) return nullptr;
   }
-  *out = &c;
+  *rc = ANNETY_CRC_OK;
+  return &c;
+}
+
+// The context of the device a call runs on: the current device, which must also own `stream`. A stream
+// of another device is refused (ANNETY_CRC_EINVAL) rather than given this device's tables and scratch:
+// a process driving several GPUs from one thread must hipSetDevice to the stream's device first. The NULL
+// stream and the per-thread / legacy handles belong to the current device by definition.
+bool special_stream(hipStream_t s) { return s == nullptr || s == hipStreamPerThread || s == hipStreamLegacy; }
+
+int stream_ctx(hipStream_t stream, DeviceCtx** out) {
+  int dev = 0;
+  HIP_TRY(hipGetDevice(&dev));
+  if (!special_stream(stream)) {
+    hipDevice_t sdev = -1;
+    const hipError_t e = hipStreamGetDevice(stream, &sdev);
+    if (e != hipSuccess) {
+      t_last_hip = static_cast<int>(e);
+      (void)hipGetLastError();
+      return ANNETY_CRC_EINVAL;  // not a stream handle
+    }
+    if (sdev != dev) return ANNETY_CRC_EINVAL;
+  }
+  int rc = 0;
+  DeviceCtx* c = ensure_ctx(dev, &rc);
+  if (!c) return rc;
+  *out = c;
   return ANNETY_CRC_OK;
 }
 
@@ -454,41 +495,51 @@ int run_var(DeviceCtx& c, const void* d_base, size_t n, uint64_t fstride, uint32
   return ANNETY_CRC_OK;
 }
 
-// Per-call device scratch of the arena, split and sorted paths: the slot this stream used last (stream
-// order fences it), else a new one (up to 8), else one taken over from another stream after
-// hipDeviceSynchronize (a ninth concurrent stream; rare). The caller holds c.arena_mu from here until its
-// launches are enqueued, then calls scratch_done. No per-call event: recording one after each call cost
-// 2-4 us of GPU time per call (a marker between one call's last kernel and the next call's first; config 3
-// 0.2111-0.2173 vs 0.2068-0.2089 ms per step, profiles/r02/arena_events_ab/). ANNETY_CRC_ARENA_EVENTS=1
-// restores the per-call event fence (any slot whose last use has finished can serve any stream), for A/B
-// runs. The stream-ordered allocator (hipMallocAsync/hipFreeAsync per call) cost ~3.6 us per call.
-bool scratch_events() {
-  static const bool events = [] {
-    const char* e = std::getenv("ANNETY_CRC_ARENA_EVENTS");
-    return e && e[0] == '1';
+// Per-call device scratch of the arena, split and sorted paths, one slot per stream, reused in stream
+// order with no per-call event (recording one after each call cost 2-4 us of GPU time per call: config 3
+// 0.2111-0.2173 vs 0.2068-0.2089 ms per step, profiles/r02/arena_events_ab/; the stream-ordered allocator
+// per call cost ~3.6 us). Slots are keyed by stream handle, and for hipStreamPerThread also by calling
+// thread (that one handle names a different stream in every thread). Up to stream_slot_cap() slots per
+// device (ANNETY_CRC_STREAM_SLOTS, default 64); past that the least recently used slot is handed over:
+// an event recorded on its last stream at that moment, waited by the new stream (hipStreamWaitEvent), so
+// no host thread and no other stream ever waits for the hand-over. The caller holds c.arena_mu from here
+// until its launches are enqueued, then calls scratch_done.
+size_t stream_slot_cap() {
+  static const size_t cap = [] {
+    const char* e = std::getenv("ANNETY_CRC_STREAM_SLOTS");
+    const long v = e && *e ? std::atol(e) : 64;
+    return (size_t)std::max(1L, std::min(4096L, v));
   }();
-  return events;
+  return cap;
+}
+
+bool same_owner(const DeviceCtx::ScratchSlot& s, hipStream_t stream) {
+  return s.last == stream && (stream != hipStreamPerThread || s.tid == std::this_thread::get_id());
 }
 
 int scratch_slot(DeviceCtx& c, hipStream_t stream, size_t bytes, DeviceCtx::ScratchSlot** out) {
-  const bool events = scratch_events();
   DeviceCtx::ScratchSlot* slot = nullptr;
-  for (int i = 0; i < c.arena_slots && !slot; i++)
-    if (c.arena_slot[i].used && c.arena_slot[i].last == stream) slot = &c.arena_slot[i];
-  if (events)
-    for (int i = 0; i < c.arena_slots && !slot; i++)
-      if (hipEventQuery(c.arena_slot[i].done) == hipSuccess) slot = &c.arena_slot[i];
-  if (!slot && c.arena_slots < 8) {
-    DeviceCtx::ScratchSlot& fresh = c.arena_slot[c.arena_slots];
-    HIP_TRY(hipEventCreateWithFlags(&fresh.done, hipEventDisableTiming));
-    c.arena_slots++;
-    slot = &fresh;
+  for (auto& s : c.slots)
+    if (same_owner(*s, stream)) {
+      slot = s.get();
+      break;
+    }
+  if (!slot && c.slots.size() < stream_slot_cap()) {
+    auto fresh = std::make_unique<DeviceCtx::ScratchSlot>();
+    HIP_TRY(hipEventCreateWithFlags(&fresh->fence, hipEventDisableTiming));
+    slot = fresh.get();
+    c.slots.push_back(std::move(fresh));
+  } else if (!slot) {
+    // hand the least recently used slot over: the new stream waits for everything its last stream had
+    // queued so far (which includes that stream's last use of the slot)
+    slot = c.slots.front().get();
+    for (auto& s : c.slots)
+      if (s->tick < slot->tick) slot = s.get();
+    if (slot->last != hipStreamPerThread) HIP_TRY(hipEventRecord(slot->fence, slot->last));
+    // a per-thread slot's fence was recorded by its own thread after its last call (scratch_done)
+    HIP_TRY(hipStreamWaitEvent(stream, slot->fence, 0));
+    c.handoffs++;
   }
-  if (!slot) {
-    slot = &c.arena_slot[c.arena_evict++ % 8];
-    if (!events) HIP_TRY(hipDeviceSynchronize());  // every earlier use of the slot has finished
-  }
-  if (events && slot->used && slot->last != stream) HIP_TRY(hipStreamWaitEvent(stream, slot->done, 0));
   if (slot->bytes < bytes) {
     if (slot->ptr) HIP_TRY(hipFreeAsync(slot->ptr, stream));
     slot->ptr = nullptr;
@@ -496,16 +547,19 @@ int scratch_slot(DeviceCtx& c, hipStream_t stream, size_t bytes, DeviceCtx::Scra
     HIP_TRY(hipMallocAsync(&slot->ptr, bytes, stream));
     slot->bytes = bytes;
   }
+  slot->last = stream;
+  slot->tid = std::this_thread::get_id();
+  slot->tick = ++c.tick;
   *out = slot;
   return ANNETY_CRC_OK;
 }
 
-// After the call's launches on `stream` (arena_mu still held): the slot's last user.
+// After the call's launches on `stream` (arena_mu still held). hipStreamPerThread resolves to the calling
+// thread's stream, which no other thread can name when it takes the slot over: such slots record their
+// fence after every call (the 2-4 us marker, paid only by callers that use the per-thread handle).
 int scratch_done(DeviceCtx::ScratchSlot* slot, hipStream_t stream) {
-  slot->last = stream;
-  slot->used = true;
-  if (!scratch_events()) return ANNETY_CRC_OK;
-  const hipError_t r = hipEventRecord(slot->done, stream);
+  if (stream != hipStreamPerThread) return ANNETY_CRC_OK;
+  const hipError_t r = hipEventRecord(slot->fence, stream);
   return r == hipSuccess ? ANNETY_CRC_OK : hip_fail(r);
 }
 
@@ -591,18 +645,21 @@ bool fixed_fast_ok(const void* d_base, size_t len, size_t stride) {
 constexpr uint64_t kSegBytes = 65536;  // 512 lines: 16 rounds of a 32-lane group
 constexpr uint32_t kMaxSegs = 16384;
 
-// Tuning/test knobs, read per call: ANNETY_CRC_SPLIT=0 never splits, =1 splits whenever the payload
-// spans two segments, unset = auto; ANNETY_CRC_SEG overrides the minimum segment size (power of two).
-int split_mode() {
+// Split policy (annety_crc_set_split; the environment's ANNETY_CRC_SPLIT / ANNETY_CRC_SEG give the initial
+// values, read once): mode 0 never splits, 1 splits whenever the payload spans two segments, -1 = auto;
+// min_segment = the smallest segment size (a power of two >= 4096). Atomics: no getenv per call, and a
+// setter racing with a call is harmless (either policy gives the same digests).
+std::atomic<int> g_split_mode{[] {
   const char* e = std::getenv("ANNETY_CRC_SPLIT");
   return e && *e ? std::atoi(e) : -1;
-}
-
-uint64_t split_min_segment() {
+}()};
+std::atomic<uint64_t> g_split_seg{[] {
   const char* e = std::getenv("ANNETY_CRC_SEG");
   const unsigned long long v = e && *e ? std::strtoull(e, nullptr, 10) : 0;
   return v >= 4096 && (v & (v - 1)) == 0 ? (uint64_t)v : kSegBytes;
-}
+}()};
+int split_mode() { return g_split_mode.load(std::memory_order_relaxed); }
+uint64_t split_min_segment() { return g_split_seg.load(std::memory_order_relaxed); }
 
 // Segment size for a fixed-length batch, or 0 to run payloads whole.
 uint64_t split_segment(size_t n, uint64_t len, int cus) {
@@ -715,13 +772,6 @@ int annety_crc_shutdown(void) {
     if (!c.ready) continue;
     (void)hipSetDevice(d);
     std::lock_guard<std::mutex> sl(c.stg_mu);
-    (void)hipFree(c.d_slice);
-    (void)hipFree(c.d_groups);
-    (void)hipFree(c.d_unshift);
-    (void)hipFree(c.d_short);
-    (void)hipFree(c.d_sb);
-    (void)hipFree(c.d_stitch);
-    (void)hipFree(c.d_zero);
     for (int i = 0; i < 2; i++) {
       if (c.stg.stream[i]) (void)hipStreamDestroy(c.stg.stream[i]);
       if (c.stg.done[i]) (void)hipEventDestroy(c.stg.done[i]);
@@ -740,19 +790,18 @@ int annety_crc_shutdown(void) {
     }
     {
       std::lock_guard<std::mutex> al(c.arena_mu);
-      if (c.arena_slots) (void)hipDeviceSynchronize();  // slots carry no event per call: drain their last uses
-      for (int i = 0; i < c.arena_slots; i++) {
-        DeviceCtx::ScratchSlot& sl = c.arena_slot[i];
-        (void)hipEventSynchronize(sl.done);
-        if (sl.ptr) (void)hipFree(sl.ptr);
-        (void)hipEventDestroy(sl.done);
-        sl = DeviceCtx::ScratchSlot{};
+      // shutdown is the one place that drains the device: the slots' last uses carry no event
+      if (!c.slots.empty()) {
+        (void)hipDeviceSynchronize();
+        c.device_syncs++;
       }
-      c.arena_slots = 0;
+      for (auto& sl : c.slots) {
+        if (sl->ptr) (void)hipFree(sl->ptr);
+        (void)hipEventDestroy(sl->fence);
+      }
+      c.slots.clear();
     }
-    c.d_slice = c.d_groups = nullptr;
-    c.d_unshift = c.d_short = nullptr;
-    c.d_sb = c.d_stitch = c.d_zero = nullptr;
+    free_images(c);
     c.ready = false;
   }
   (void)hipSetDevice(prev);
@@ -776,6 +825,44 @@ int annety_crc_last_hip_error(void) { return t_last_hip; }
 int annety_crc_reserve_cus(int n) {
   if (n < 0) return ANNETY_CRC_EINVAL;
   g_reserved_cus.store(n);
+  return ANNETY_CRC_OK;
+}
+
+int annety_crc_set_split(int mode, uint64_t min_segment) {
+  if (mode < -1 || mode > 1) return ANNETY_CRC_EINVAL;
+  if (min_segment && (min_segment < 4096 || (min_segment & (min_segment - 1)))) return ANNETY_CRC_EINVAL;
+  g_split_mode.store(mode);
+  g_split_seg.store(min_segment ? min_segment : kSegBytes);
+  return ANNETY_CRC_OK;
+}
+
+int annety_crc_scratch_stats(int device, uint64_t* slots, uint64_t* handoffs, uint64_t* device_syncs) {
+  if (device < 0 || device >= kMaxDev) return ANNETY_CRC_ENODEV;
+  DeviceCtx& c = g_dev[device];
+  {
+    std::lock_guard<std::mutex> lk(c.arena_mu);
+    if (slots) *slots = c.slots.size();
+  }
+  if (handoffs) *handoffs = c.handoffs.load();
+  if (device_syncs) *device_syncs = c.device_syncs.load();
+  return ANNETY_CRC_OK;
+}
+
+int annety_crc_stream_release(void* stream) {
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  DeviceCtx* c = nullptr;
+  int rc = stream_ctx(s, &c);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(c->arena_mu);
+  for (size_t i = 0; i < c->slots.size(); i++) {
+    DeviceCtx::ScratchSlot& sl = *c->slots[i];
+    if (!same_owner(sl, s)) continue;
+    // stream-ordered: the memory returns to the pool after the stream's queued work, nobody waits
+    if (sl.ptr) HIP_TRY(hipFreeAsync(sl.ptr, s));
+    (void)hipEventDestroy(sl.fence);
+    c->slots.erase(c->slots.begin() + (long)i);
+    break;
+  }
   return ANNETY_CRC_OK;
 }
 
@@ -818,7 +905,7 @@ int annety_crc32_batch_fixed(const void* d_base, size_t n, size_t len, size_t st
   if (n == 0) return ANNETY_CRC_OK;
   if (!d_out || (!d_base && len > 0) || (n > 1 && stride < len)) return ANNETY_CRC_EINVAL;
   DeviceCtx* c = nullptr;
-  int rc = current_ctx(&c);
+  int rc = stream_ctx(static_cast<hipStream_t>(stream), &c);
   if (rc) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (len == 0) {
@@ -838,7 +925,7 @@ int annety_crc32_batch_var(const void* d_base, const uint64_t* d_off, const uint
   if (n == 0) return ANNETY_CRC_OK;
   if (!d_base || !d_off || !d_len || !d_out) return ANNETY_CRC_EINVAL;
   DeviceCtx* c = nullptr;
-  int rc = current_ctx(&c);
+  int rc = stream_ctx(static_cast<hipStream_t>(stream), &c);
   if (rc) return rc;
   if (n > 0xFFFFFFFFull) return ANNETY_CRC_EINVAL;  // order[] holds 32-bit payload indices
   return run_var_sorted(*c, d_base, n, d_off, d_len, d_out, static_cast<hipStream_t>(stream));
@@ -849,7 +936,7 @@ int annety_crc32_batch_var_arena(const void* d_arena, size_t arena_bytes, const 
   if (n == 0) return ANNETY_CRC_OK;
   if (!d_arena || !d_off || !d_len || !d_out) return ANNETY_CRC_EINVAL;
   DeviceCtx* c = nullptr;
-  int rc = current_ctx(&c);
+  int rc = stream_ctx(static_cast<hipStream_t>(stream), &c);
   if (rc) return rc;
   return run_arena(*c, d_arena, arena_bytes, d_off, d_len, n, d_out, static_cast<hipStream_t>(stream), false);
 }
@@ -859,7 +946,7 @@ int annety_crc32_update_batch_var_arena(uint32_t* d_state, const void* d_arena, 
   if (n == 0) return ANNETY_CRC_OK;
   if (!d_state || !d_arena || !d_off || !d_len) return ANNETY_CRC_EINVAL;
   DeviceCtx* c = nullptr;
-  int rc = current_ctx(&c);
+  int rc = stream_ctx(static_cast<hipStream_t>(stream), &c);
   if (rc) return rc;
   return run_arena(*c, d_arena, arena_bytes, d_off, d_len, n, d_state, static_cast<hipStream_t>(stream), true);
 }
@@ -870,7 +957,7 @@ int annety_crc32_update_batch_fixed(uint32_t* d_state, const void* d_base, size_
   if (!d_state || !d_base || (n > 1 && stride < len)) return ANNETY_CRC_EINVAL;
   if (len > 0xFFFFFFFFull) return ANNETY_CRC_EINVAL;
   DeviceCtx* c = nullptr;
-  int rc = current_ctx(&c);
+  int rc = stream_ctx(static_cast<hipStream_t>(stream), &c);
   if (rc) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
   if (fixed_fast_ok(d_base, len, stride)) return run_fixed(*c, d_base, n, len, stride, d_state, true, s);
@@ -886,7 +973,7 @@ int annety_crc32_update_batch_var(uint32_t* d_state, const void* d_base, const u
   if (!d_state || !d_base || !d_off || !d_len) return ANNETY_CRC_EINVAL;
   if (n > 0xFFFFFFFFull) return ANNETY_CRC_EINVAL;
   DeviceCtx* c = nullptr;
-  int rc = current_ctx(&c);
+  int rc = stream_ctx(static_cast<hipStream_t>(stream), &c);
   if (rc) return rc;
   return run_var_sorted(*c, d_base, n, d_off, d_len, d_state, static_cast<hipStream_t>(stream), true);
 }
@@ -922,7 +1009,7 @@ int annety_crc32_batch_fixed_host(const void* h_base, size_t n, size_t len, size
     return ANNETY_CRC_OK;
   }
   DeviceCtx* c = nullptr;
-  int rc = current_ctx(&c);
+  int rc = stream_ctx(nullptr, &c);
   if (rc) return rc;
   std::lock_guard<std::mutex> lk(c->stg_mu);
   Staging& st = c->stg;
@@ -1062,7 +1149,7 @@ static int lhc_verify(const void* d_stream, size_t stream_bytes, bool arena, con
   if (n == 0) return ANNETY_CRC_OK;
   if (!d_stream || !d_payload_off || !d_payload_len || !d_ok) return ANNETY_CRC_EINVAL;
   DeviceCtx* c = nullptr;
-  int rc = current_ctx(&c);
+  int rc = stream_ctx(static_cast<hipStream_t>(stream), &c);
   if (rc) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint32_t* dig = d_digest;
@@ -1115,7 +1202,7 @@ static int encode_batch(const FrameRules& r, const void* d_src, const uint64_t* 
   if (n == 0) return ANNETY_CRC_OK;
   if (!lhc_type_ok(r.T) || !d_src || !d_src_off || !d_len || !d_dst || !d_frame_off) return ANNETY_CRC_EINVAL;
   DeviceCtx* c = nullptr;
-  int rc = current_ctx(&c);
+  int rc = stream_ctx(static_cast<hipStream_t>(stream), &c);
   if (rc) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
   uint32_t* dig = nullptr;
@@ -1163,7 +1250,7 @@ static int verify_host(const FrameRules& r, const void* h_stream, size_t size, u
   if (size == 0 || max_frames == 0)
     return parse_frames(r, h_stream, size, h_payload_off, h_payload_len, max_frames, n_frames, consumed);
   DeviceCtx* c = nullptr;
-  int rc = current_ctx(&c);
+  int rc = stream_ctx(nullptr, &c);
   if (rc) return rc;
   std::lock_guard<std::mutex> lk(c->stg_mu);
   Staging& st = c->stg;

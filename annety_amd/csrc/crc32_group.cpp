@@ -6,7 +6,10 @@
 //  * annety_crc32_group_batch_fixed: device-resident shards; each device checksums its shard chunk by
 //    chunk on its own stream, and chunk c's digests travel to the root device over RCCL (xGMI) on a
 //    communication stream while chunk c+1 is computed. The communicator is ncclCommInitAll over the
-//    group's devices (single process); send/recv pairs are fused in ncclGroupStart/End.
+//    group's devices (single process); send/recv pairs are fused in ncclGroupStart/End. The pieces and
+//    their destinations come from annety_crc_group_schedule (host only, CPU-tested for 8 devices).
+//    UNVERIFIED ON HARDWARE: with one device nothing is sent (the root computes in place), so the
+//    send/recv branch runs only on a multi-GPU box, which the test pool does not provide.
 //  * annety_crc32_group_batch_fixed_host: a host batch split over the devices, each share staged over
 //    its own device's PCIe link by one host thread (annety_crc32_batch_fixed_host per device).
 // Built on the single-device entry points; every call restores the caller's current device.
@@ -137,6 +140,23 @@ int annety_crc_group_destroy(annety_crc_group* g) {
 
 int annety_crc_group_size(const annety_crc_group* g) { return g ? (int)g->dev.size() : 0; }
 
+int annety_crc_group_schedule(const size_t* n_shard, int nd, size_t chunks, size_t* plan) {
+  if (!n_shard || nd <= 0 || chunks == 0 || !plan) return ANNETY_CRC_EINVAL;
+  size_t base = 0;
+  for (int k = 0; k < nd; k++) {
+    for (size_t c = 0; c < chunks; c++) {
+      size_t lo, hi;
+      chunk_of(n_shard[k], chunks, c, &lo, &hi);
+      size_t* e = plan + (c * (size_t)nd + (size_t)k) * 3;
+      e[0] = lo;         // first payload of the piece, within shard k
+      e[1] = hi - lo;    // payloads in the piece (0: nothing to compute or move)
+      e[2] = base + lo;  // where its digests land in the root's output
+    }
+    base += n_shard[k];
+  }
+  return ANNETY_CRC_OK;
+}
+
 int annety_crc32_group_batch_fixed(annety_crc_group* g, const void* const* d_shard, const size_t* n_shard, size_t len,
                                    size_t stride, uint32_t* d_root_out, size_t chunks) {
   if (!g || !d_shard || !n_shard || !d_root_out) return ANNETY_CRC_EINVAL;
@@ -148,12 +168,12 @@ int annety_crc32_group_batch_fixed(annety_crc_group* g, const void* const* d_sha
     total += n_shard[k];
   }
   if (total == 0) return ANNETY_CRC_OK;
-  chunks = std::max<size_t>(1, chunks);
+  chunks = std::max<size_t>(1, std::min(chunks, total));
+  std::vector<size_t> plan(chunks * (size_t)nd * 3);
+  (void)annety_crc_group_schedule(n_shard, nd, chunks, plan.data());
   std::lock_guard<std::mutex> lk(g->mu);
   DeviceGuard guard;
   // digests of device k land at d_root_out + base[k] (root) or in its scratch (others), then move to root
-  std::vector<size_t> base(nd, 0);
-  for (int k = 1; k < nd; k++) base[k] = base[k - 1] + n_shard[k - 1];
   for (int k = 1; k < nd; k++) {
     if (g->scratch_cap[k] < n_shard[k]) {
       GHIP(hipSetDevice(g->dev[k]));
@@ -164,44 +184,54 @@ int annety_crc32_group_batch_fixed(annety_crc_group* g, const void* const* d_sha
       g->scratch_cap[k] = n_shard[k];
     }
   }
-  for (size_t c = 0; c < chunks; c++) {
-    // compute chunk c on every device
-    for (int k = 0; k < nd; k++) {
-      size_t lo, hi;
-      chunk_of(n_shard[k], chunks, c, &lo, &hi);
-      if (hi == lo) continue;
-      GHIP(hipSetDevice(g->dev[k]));
-      uint32_t* dst = (k == 0 ? d_root_out + base[0] : g->scratch[k]) + lo;
-      const int rc = annety_crc32_batch_fixed(static_cast<const char*>(d_shard[k]) + lo * stride, hi - lo, len, stride,
-                                              dst, g->compute[k]);
-      if (rc) return rc;
-      GHIP(hipEventRecord(g->ready[k], g->compute[k]));
-      GHIP(hipStreamWaitEvent(g->comms[k], g->ready[k], 0));
-    }
-    // move chunk c of every other shard to the root while chunk c+1 computes
-    if (nd > 1) {
-      GNCCL(ncclGroupStart());
-      for (int k = 1; k < nd; k++) {
-        size_t lo, hi;
-        chunk_of(n_shard[k], chunks, c, &lo, &hi);
-        if (hi == lo) continue;
-        if (ncclSend(g->scratch[k] + lo, hi - lo, ncclUint32, 0, g->comm[k], g->comms[k]) != ncclSuccess ||
-            ncclRecv(d_root_out + base[k] + lo, hi - lo, ncclUint32, k, g->comm[0], g->comms[0]) != ncclSuccess) {
-          (void)ncclGroupEnd();
-          return ANNETY_CRC_ERCCL;
-        }
+  // Everything is enqueued here; on any failure part of it may already be queued (kernels writing the
+  // scratch, sends reading it), so every stream of the group is drained before the mutex is released and
+  // the next call may reuse the scratch.
+  auto enqueue = [&]() -> int {
+    for (size_t c = 0; c < chunks; c++) {
+      // compute piece c of every shard
+      for (int k = 0; k < nd; k++) {
+        const size_t* e = &plan[(c * (size_t)nd + (size_t)k) * 3];
+        if (!e[1]) continue;
+        GHIP(hipSetDevice(g->dev[k]));
+        uint32_t* dst = k == 0 ? d_root_out + e[2] : g->scratch[k] + e[0];
+        const int rc = annety_crc32_batch_fixed(static_cast<const char*>(d_shard[k]) + e[0] * stride, e[1], len, stride,
+                                                dst, g->compute[k]);
+        if (rc) return rc;
+        if (k == 0) continue;  // the root's digests are already in place
+        GHIP(hipEventRecord(g->ready[k], g->compute[k]));
+        GHIP(hipStreamWaitEvent(g->comms[k], g->ready[k], 0));  // the send waits for its piece's kernel
       }
-      GNCCL(ncclGroupEnd());
+      // move piece c of every other shard to the root while piece c+1 computes: one send/recv pair per
+      // device (rank k of the communicator -> rank 0), fused in one group so the root's receives from all
+      // peers progress together; the root never sends to itself
+      if (nd > 1) {
+        GNCCL(ncclGroupStart());
+        int bad = 0;
+        for (int k = 1; k < nd && !bad; k++) {
+          const size_t* e = &plan[(c * (size_t)nd + (size_t)k) * 3];
+          if (!e[1]) continue;
+          bad = ncclSend(g->scratch[k] + e[0], e[1], ncclUint32, 0, g->comm[k], g->comms[k]) != ncclSuccess ||
+                ncclRecv(d_root_out + e[2], e[1], ncclUint32, k, g->comm[0], g->comms[0]) != ncclSuccess;
+        }
+        if (ncclGroupEnd() != ncclSuccess || bad) return ANNETY_CRC_ERCCL;
+      }
     }
-  }
-  for (int k = 0; k < nd; k++) {
-    GHIP(hipSetDevice(g->dev[k]));
-    GHIP(hipStreamSynchronize(g->compute[k]));
-    GHIP(hipStreamSynchronize(g->comms[k]));
+    return ANNETY_CRC_OK;
+  };
+  int rc = enqueue();
+  for (int k = 0; k < nd; k++) {  // drain every stream, also after a failure
+    if (hipSetDevice(g->dev[k]) != hipSuccess) {
+      if (!rc) rc = ANNETY_CRC_EHIP;
+      continue;
+    }
+    const hipError_t e1 = hipStreamSynchronize(g->compute[k]);
+    const hipError_t e2 = hipStreamSynchronize(g->comms[k]);
+    if (!rc && (e1 != hipSuccess || e2 != hipSuccess)) rc = hip_status(e1 != hipSuccess ? e1 : e2);
     ncclResult_t async = ncclSuccess;
-    if (ncclCommGetAsyncError(g->comm[k], &async) != ncclSuccess || async != ncclSuccess) return ANNETY_CRC_ERCCL;
+    if (!rc && (ncclCommGetAsyncError(g->comm[k], &async) != ncclSuccess || async != ncclSuccess)) rc = ANNETY_CRC_ERCCL;
   }
-  return ANNETY_CRC_OK;
+  return rc;
 }
 
 int annety_crc32_group_batch_fixed_host(annety_crc_group* g, const void* h_base, size_t n, size_t len, size_t stride,

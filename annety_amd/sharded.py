@@ -172,6 +172,21 @@ def shard_plan(n: int, nshards: int) -> list:
     return [(int(first[k]), int(count[k])) for k in range(nshards)]
 
 
+def group_schedule(n_shard, chunks: int) -> list:
+    """annety_crc_group_schedule: for piece c of shard k, plan[c][k] = (first payload within the shard,
+    payload count, index of its first digest in the root's output) - what annety_crc32_group_batch_fixed
+    computes and sends."""
+    import ctypes
+
+    from . import _lib
+
+    nd = len(n_shard)
+    ns = (ctypes.c_size_t * nd)(*n_shard)
+    plan = (ctypes.c_size_t * (chunks * nd * 3))()
+    _lib.check(_lib.get().annety_crc_group_schedule(ns, nd, chunks, plan), "annety_crc_group_schedule")
+    return [[tuple(int(plan[(c * nd + k) * 3 + i]) for i in range(3)) for k in range(nd)] for c in range(chunks)]
+
+
 class DeviceGroup:
     """One process driving several devices (annety_crc_group): device-resident shards with the digests
     gathered to devices[0] over RCCL, or a host batch staged over every device's PCIe link."""

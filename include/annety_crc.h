@@ -13,10 +13,17 @@
  * Error model (the reference functions are total): every entry point that can fail
  * returns an int status, 0 on success, a negative ANNETY_CRC_E* code otherwise, and never aborts.
  * Thread safety: all entry points are reentrant; device state is initialised once per device.
+ * Devices: device entry points run on the CURRENT device (hipSetDevice), and `stream` must belong to it:
+ * a stream of another device returns ANNETY_CRC_EINVAL (never another device's tables). NULL,
+ * hipStreamPerThread and hipStreamLegacy name streams of the current device. A process driving several
+ * GPUs from one thread sets the device to the stream's before each call (or uses the device groups below).
  * Streams: the variable, arena and split paths keep per-call device scratch per (device, stream), reused
- * in stream order. Up to 8 streams per device hold their own; a further stream takes one over after a
- * device-wide synchronise. Do not destroy a stream while a call on it is still running and then pass a
- * new stream that reuses its handle: that is a race, as it is with any stream-ordered resource.
+ * in stream order with no per-call event and no host wait (hipStreamPerThread is keyed per calling
+ * thread, since that handle names a different stream in every thread). Up to 64 streams per device
+ * (ANNETY_CRC_STREAM_SLOTS) hold their own; past that, the least recently used stream's scratch is
+ * handed over by an event recorded on that stream and waited by the new one (no device-wide sync, no
+ * host block). A stream that has used these paths must stay valid until annety_crc_stream_release(stream)
+ * (or annety_crc_shutdown): call it before hipStreamDestroy.
  */
 #ifndef ANNETY_CRC_H
 #define ANNETY_CRC_H
@@ -28,7 +35,7 @@
 extern "C" {
 #endif
 
-#define ANNETY_CRC_ABI_VERSION 2
+#define ANNETY_CRC_ABI_VERSION 3
 
 enum {
   ANNETY_CRC_OK = 0,
@@ -53,6 +60,17 @@ int annety_crc_last_hip_error(void);
  * that work on other streams - e.g. the RCCL kernels of a digest gather overlapped with the next chunk -
  * runs beside them instead of between them. 0 (default) uses every CU. Process-wide. */
 int annety_crc_reserve_cus(int n);
+/* Long-payload split policy, process-wide (initial values from ANNETY_CRC_SPLIT / ANNETY_CRC_SEG, read
+ * once): mode -1 = auto (split when the batch is too small to fill the chip), 0 = never, 1 = whenever a
+ * payload spans two segments; min_segment = smallest segment in bytes (power of two >= 4096), 0 = default
+ * 64 KiB. Digests do not depend on it. */
+int annety_crc_set_split(int mode, uint64_t min_segment);
+/* Drops `stream`'s per-stream scratch on the current device (stream-ordered free, no wait). Call before
+ * destroying a stream that ran variable, arena or split batches. */
+int annety_crc_stream_release(void* stream);
+/* Scratch bookkeeping of `device` (test and tuning visibility): streams holding a slot, hand-overs of a
+ * slot between streams so far, device-wide synchronisations so far (0 outside annety_crc_shutdown). */
+int annety_crc_scratch_stats(int device, uint64_t* slots, uint64_t* handoffs, uint64_t* device_syncs);
 
 /* ---- host scalar API: exact replacements of the reference's inline methods ----
  * annety_crc32_long   replaces Crc32c::crc32_long(const char*, size_t)   include/Crc32c.h:58-69
@@ -121,6 +139,11 @@ typedef struct annety_crc_group annety_crc_group;
 /* Contiguous block shards of n payloads over nshards: shard k = [first[k], first[k] + count[k]), sizes
  * within one of each other. Host only (no device needed). */
 int annety_crc_shard_plan(size_t n, int nshards, size_t* first, size_t* count);
+/* The transfer schedule annety_crc32_group_batch_fixed runs (host only): shard k is cut into `chunks`
+ * near-equal pieces; for piece c of shard k, plan[(c*nd + k)*3 + 0] = its first payload within the shard,
+ * [+1] = its payload count (0: nothing to do), [+2] = the index in d_root_out where its digests land
+ * (sum(n_shard[0..k-1]) + first). plan holds chunks*nd*3 entries. */
+int annety_crc_group_schedule(const size_t* n_shard, int nd, size_t chunks, size_t* plan);
 /* ANNETY_CRC_ENODEV if a device is missing or not gfx950, ANNETY_CRC_EINVAL for a repeated device,
  * ANNETY_CRC_ERCCL if the communicator cannot be built. */
 int annety_crc_group_create(const int* devices, int ndev, annety_crc_group** out);

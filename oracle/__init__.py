@@ -270,6 +270,9 @@ def ref_lib() -> ctypes.CDLL:
         lib.ref_crc32_batch_fixed_mt.restype = ctypes.c_int
         lib.ref_crc32_batch_fixed_mt.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t,
                                                  ctypes.c_void_p, ctypes.c_int]
+        lib.ref_crc32_batch_var_mt.restype = ctypes.c_int
+        lib.ref_crc32_batch_var_mt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+                                               ctypes.c_void_p, ctypes.c_int]
         _ref = lib
     return _ref
 

@@ -165,3 +165,57 @@ def test_group_errors_without_device():
     assert lib.annety_crc_group_size(None) == 0
     assert lib.annety_crc_group_destroy(None) == 0
     assert lib.annety_crc32_group_batch_fixed(None, None, None, 16, 16, None, 1) == -1
+
+
+def test_group_schedule_eight_devices():
+    """The transfer schedule of annety_crc32_group_batch_fixed (annety_crc_group_schedule, the same
+    arithmetic the send/recv loop runs) for 8 devices: every payload of the batch is computed exactly once
+    and its digest lands at its global index in the root's output; pieces tile each shard in order; a
+    device's piece c is the same on the sending and the receiving side."""
+    from annety_amd import sharded
+
+    lib = _lib.get()
+    assert lib.annety_crc_group_schedule(None, 8, 2, None) == -1
+    for n in [1, 7, 8, 1000, 1001, 64 << 20]:
+        shards = sharded.shard_plan(n, 8)
+        counts = [c for _, c in shards]
+        for chunks in [1, 2, 3, 8, 13]:
+            plan = sharded.group_schedule(counts, chunks)
+            seen = np.zeros(n, dtype=np.int8) if n < (1 << 20) else None
+            for k in range(8):
+                pos = 0
+                for c in range(chunks):
+                    lo, cnt, dst = plan[c][k]
+                    assert lo == pos  # pieces tile shard k in order
+                    assert dst == shards[k][0] + lo  # global index = shard start + offset in the shard
+                    pos += cnt
+                    if seen is not None:
+                        seen[dst:dst + cnt] += 1
+                assert pos == counts[k]
+                sizes = [plan[c][k][1] for c in range(chunks)]
+                assert max(sizes) - min(sizes) <= 1  # near-equal pieces
+            if seen is not None:
+                assert (seen == 1).all()
+
+
+def test_boundary_error_paths_without_device():
+    """Error paths of the entry points added for multi-stream / multi-device callers, on a host with no
+    GPU: argument checks come first, and a call that needs a device reports it instead of crashing."""
+    import ctypes
+
+    lib = _lib.get()
+    assert lib.annety_crc_set_split(2, 0) == -1  # mode out of range
+    assert lib.annety_crc_set_split(1, 5000) == -1  # segment not a power of two
+    assert lib.annety_crc_set_split(1, 1024) == -1  # segment below 4 KiB
+    assert lib.annety_crc_set_split(-1, 0) == 0
+    v = [ctypes.c_uint64(7) for _ in range(3)]
+    assert lib.annety_crc_scratch_stats(-1, *[ctypes.byref(x) for x in v]) == -4
+    assert lib.annety_crc_scratch_stats(0, *[ctypes.byref(x) for x in v]) == 0
+    assert [x.value for x in v] == [0, 0, 0]  # nothing ran on device 0 in this process
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        buf = (ctypes.c_uint8 * 64)()
+        out = (ctypes.c_uint32 * 4)()
+        # valid arguments, no device: a negative status (no HIP device), never a crash
+        assert lib.annety_crc32_batch_fixed(ctypes.addressof(buf), 4, 16, 16, ctypes.addressof(out), None) < 0
+        assert lib.annety_crc_stream_release(None) < 0

@@ -1,9 +1,11 @@
 """Per-call scratch across streams (crc32_capi.cpp scratch_slot: arena, sorted and split paths): each
-stream keeps its own scratch slot, fenced by stream order; a ninth stream takes a slot over after a
-device synchronise. Eleven streams
-(more than the 8 slots) interleave arena batches of different sizes, several rounds each, and every
-digest is compared with the oracle. Batches are packed Zipf-like lengths at unaligned starts, so every
-call runs the line pass and the stitch (the path of BASELINE config 3)."""
+stream keeps its own scratch slot, fenced by stream order; past the slot cap (ANNETY_CRC_STREAM_SLOTS,
+default 64) the least recently used slot is handed over by an event recorded on its last stream - never
+a device-wide synchronise (annety_crc_scratch_stats counts them). Streams interleave arena batches of
+different sizes, several rounds each, and every digest is compared with the oracle. Batches are packed
+Zipf-like lengths at unaligned starts, so every call runs the line pass and the stitch (the path of
+BASELINE config 3). hipStreamPerThread, one handle naming a different stream per thread, gets a slot
+per calling thread."""
 import numpy as np
 import pytest
 
@@ -98,3 +100,136 @@ def test_sorted_and_split_paths_across_streams(gpu):
         for r in range(rounds):
             got = outs[i][r].cpu().numpy().view(np.uint32)
             assert np.array_equal(got, want), f"{kind} stream {i} round {r}: {int((got != want).sum())} differ"
+
+
+def _arena_job(gpu, seed, total):
+    import torch
+
+    data, offs, lens = _batch(seed, total)
+    want = oracle.batch_var(data, offs.astype(np.uint64), lens.astype(np.uint32))
+    return (torch.from_numpy(data).to(gpu), torch.from_numpy(offs).to(gpu),
+            torch.from_numpy(lens.astype(np.int32)).to(gpu), want, len(data))
+
+
+def test_sixteen_streams_in_rotation_no_device_sync(gpu):
+    """16 streams in rotation (annety's >8 IO loops on one device): each keeps its own slot, no slot is
+    handed over and no device-wide synchronise happens; per-call cost is timed against one stream."""
+    import time
+
+    import torch
+
+    import annety_amd
+
+    before = annety_amd.scratch_stats(0)
+    streams = [torch.cuda.Stream(gpu) for _ in range(16)]
+    d, o, ln, want, nbytes = _arena_job(gpu, 4242, 1 << 20)
+    outs = [torch.empty(ln.numel(), dtype=torch.int32, device=gpu) for _ in streams]
+    torch.cuda.synchronize()
+
+    def rotate(ss, rounds):
+        for _ in range(rounds):
+            for i, st in enumerate(ss):
+                annety_amd.crc32_batch_var(d, o, ln, out=outs[i], stream=st, arena=nbytes)
+        torch.cuda.synchronize()
+
+    rotate(streams, 2)  # every stream takes its slot
+    for i in range(16):
+        assert np.array_equal(outs[i].cpu().numpy().view(np.uint32), want), i
+    after = annety_amd.scratch_stats(0)
+    assert after["device_syncs"] == before["device_syncs"] == 0
+    assert after["handoffs"] == before["handoffs"]
+    assert after["slots"] >= 16
+    # per-call time: the 16 streams in rotation against the same calls on one stream
+    t0 = time.perf_counter()
+    rotate(streams, 8)
+    t16 = (time.perf_counter() - t0) / 128
+    t0 = time.perf_counter()
+    rotate([streams[0]] * 16, 8)
+    t1 = (time.perf_counter() - t0) / 128
+    print(f"per call: 16 streams {t16 * 1e6:.1f} us, 1 stream {t1 * 1e6:.1f} us")
+    assert t16 < 3 * t1 + 100e-6
+    assert annety_amd.scratch_stats(0)["device_syncs"] == 0
+    for st in streams:
+        annety_amd.stream_release(st)
+    assert annety_amd.scratch_stats(0)["slots"] == after["slots"] - 16
+
+
+HANDOFF_SCRIPT = r"""
+import sys
+import numpy as np
+import torch
+sys.path.insert(0, {root!r})
+sys.path.insert(0, {tests!r})
+import annety_amd
+import test_gpu_arena_streams as t
+gpu = torch.device("cuda", 0)
+streams = [torch.cuda.Stream(gpu) for _ in range(11)]
+jobs = [t._arena_job(gpu, 500 + i, (1 << 19) * (1 + i % 3) + 777 * i) for i in range(11)]
+outs = [[torch.empty(j[2].numel(), dtype=torch.int32, device=gpu) for _ in range(3)] for j in jobs]
+torch.cuda.synchronize()
+for r in range(3):
+    for i, (d, o, ln, want, nb) in enumerate(jobs):
+        with torch.cuda.stream(streams[i]):
+            for x in (d, o, ln, outs[i][r]):
+                x.record_stream(streams[i])
+            annety_amd.crc32_batch_var(d, o, ln, out=outs[i][r], stream=streams[i], arena=nb)
+torch.cuda.synchronize()
+bad = sum(int((outs[i][r].cpu().numpy().view(np.uint32) != jobs[i][3]).sum()) for i in range(11) for r in range(3))
+s = annety_amd.scratch_stats(0)
+print("RESULT", bad, s["slots"], s["handoffs"], s["device_syncs"])
+"""
+
+
+def test_slot_handoff_past_the_cap(gpu, tmp_path):
+    """With the cap at 4 slots, 11 streams x 3 rounds take slots over from each other: every digest is
+    right, hand-overs happen, and none of them synchronises the device."""
+    import os
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    script = tmp_path / "handoff.py"
+    script.write_text(HANDOFF_SCRIPT.format(root=os.path.dirname(here), tests=here))
+    env = dict(os.environ, ANNETY_CRC_STREAM_SLOTS="4")
+    r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=110, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    bad, slots, handoffs, syncs = map(int, [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT")][0].split()[1:])
+    assert bad == 0 and slots == 4 and handoffs > 0 and syncs == 0
+
+
+def test_per_thread_stream_handle_two_threads(gpu):
+    """Two host threads pass the same hipStreamPerThread handle (2), which HIP resolves to each thread's
+    own stream: they get separate scratch slots, so their line passes and stitches cannot overwrite each
+    other's S/SB; every digest of every call is checked."""
+    import threading
+
+    import torch
+
+    import annety_amd
+
+    PER_THREAD = 2  # hipStreamPerThread
+    jobs = [_arena_job(gpu, 900 + k, (1 << 20) + 999 * k) for k in range(2)]
+    torch.cuda.synchronize()
+    errors = []
+
+    def worker(k):
+        try:
+            torch.cuda.set_device(gpu)
+            d, o, ln, want, nb = jobs[k]
+            for r in range(20):
+                out = torch.empty(ln.numel(), dtype=torch.int32, device=gpu)
+                annety_amd.crc32_batch_var(d, o, ln, out=out, stream=PER_THREAD, arena=nb)
+                torch.cuda.synchronize()  # the per-thread stream is not torch's; wait for the device
+                got = out.cpu().numpy().view(np.uint32)
+                if not np.array_equal(got, want):
+                    errors.append((k, r, int((got != want).sum())))
+        except Exception as e:  # noqa: BLE001
+            errors.append((k, repr(e)))
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in range(2)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join(100)
+    assert not errors, errors
+    assert annety_amd.scratch_stats(0)["device_syncs"] == 0

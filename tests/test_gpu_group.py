@@ -1,8 +1,10 @@
 """Device groups (annety_crc_group_*: single process, RCCL communicator from ncclCommInitAll) on the
 GPU box's one device: the sharded device-resident batch with the chunked digest gather to the root,
-and the host batch staged over the group's PCIe links - bit-exact against the oracle. (A one-device
-group still builds the communicator and runs the root's send/recv schedule; the 8-device gather is
-exercised by the driver's multi-GPU run of bench.py.)"""
+and the host batch staged over the group's PCIe links - bit-exact against the oracle. A one-device
+group builds the communicator but sends nothing (the root computes into its output directly): the
+grouped ncclSend/ncclRecv branch of crc32_group.cpp runs only with two or more devices, which this
+one-GPU box cannot provide, and stays unverified on hardware. Its transfer schedule is the host-only
+annety_crc_group_schedule, checked for 8 devices on the CPU (tests/test_capi.py)."""
 import numpy as np
 import pytest
 
@@ -42,21 +44,41 @@ def test_group_host_batch(gpu):
     assert np.array_equal(got, oracle.batch_fixed_mt(host, n, L, threads=8))
 
 
-def test_bench_dist_path_one_rank(gpu):
-    """bench.py's N > 1 code path at one rank over RCCL (--dist): the real kernels produce each chunk,
-    the digests (double-buffered across steps) are gathered asynchronously, the correctness gate checks
-    the rank's digests against the oracle and verify_gather checks what rank 0 received."""
+def _bench(*extra):
     import json
     import os
     import subprocess
     import sys
 
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    cmd = [sys.executable, os.path.join(root, "bench.py"), "--dist", "--config", "4", "--payloads", "65536",
-           "--steps", "4", "--warmup", "2", "--prewarm-s", "0", "--chunks", "3"]
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--steps", "4", "--warmup", "2", "--prewarm-s", "0",
+           "--no-cpu", *extra]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=110, cwd=root)
     assert r.returncode == 0, r.stderr[-2000:]
-    line = json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+    return json.loads([ln for ln in r.stdout.splitlines() if ln.startswith("{")][-1])
+
+
+def test_bench_dist_path_one_rank(gpu):
+    """bench.py's N > 1 code path at one rank over RCCL (--dist): the real kernels produce each chunk,
+    the digests (double-buffered across steps) are gathered asynchronously, the correctness gate checks
+    the rank's digests against the oracle and verify_gather checks what rank 0 received. The default
+    N > 1 workload is N = 1's (config 1 per GPU), so the driver's 1..8-GPU lines are one weak-scaling curve."""
+    line = _bench("--dist", "--payloads", "65536")
+    one = _bench("--payloads", "65536")
     assert line["rccl_ranks"] == 1 and line["backend"] == "nccl"
     assert line["gather"]["verified"] is True and line["gather"]["overlapped_across_steps"] is True
-    assert line["gather"]["chunks"] == 3 and line["n_gpus"] == 1 and line["value"] > 0
+    assert line["gather"]["chunks"] == 1 and line["n_gpus"] == 1 and line["value"] > 0
+    assert line["config"]["workload"] == one["config"]["workload"]
+    assert line["metric"] == one["metric"] and line["scaling"] == one["scaling"] == "weak"
+    assert one["ms_per_step_min"] <= one["ms_per_step_median"] <= one["ms_per_step_max"]
+    c4 = _bench("--dist", "--config", "4", "--payloads", "65536", "--chunks", "3")
+    assert c4["gather"]["chunks"] == 3 and c4["gather"]["verified"] is True and "config 4" in c4["metric"]
+
+
+def test_bench_strong_one_rank(gpu):
+    """--strong: the payload count is the job's total, split into contiguous shards; at one rank the shard
+    is the whole batch and the gather moves it to rank 0."""
+    line = _bench("--dist", "--strong", "--payloads", "50001")
+    assert line["scaling"] == "strong" and line["config"]["payloads_total"] == 50001
+    assert line["config"]["payloads_per_gpu"] == 50001 and line["gather"]["verified"] is True
+    assert "strong" in line["metric"]

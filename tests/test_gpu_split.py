@@ -1,4 +1,4 @@
-"""Long payloads through the segment + combine path (ANNETY_CRC_SPLIT; crc32_split_desc/join).
+"""Long payloads through the segment + combine path (annety_crc_set_split; crc32_split_desc/join).
 
 Each case runs with the split forced on and forced off and must give the reference's digests
 (golden fixtures) or the oracle's; the > 4 GiB payload, which only the split path accepts, is checked
@@ -19,18 +19,20 @@ def H(x: str) -> int:
 
 
 class _split:
+    """The split policy (annety_crc_set_split) for the duration of a block; back to auto after."""
+
     def __init__(self, mode: str):
-        self.mode = mode
+        self.mode = int(mode)
 
     def __enter__(self):
-        self.old = os.environ.get("ANNETY_CRC_SPLIT")
-        os.environ["ANNETY_CRC_SPLIT"] = self.mode
+        import annety_amd
+
+        annety_amd.set_split(self.mode)
 
     def __exit__(self, *a):
-        if self.old is None:
-            os.environ.pop("ANNETY_CRC_SPLIT", None)
-        else:
-            os.environ["ANNETY_CRC_SPLIT"] = self.old
+        import annety_amd
+
+        annety_amd.set_split(-1)
 
 
 def _digests(out):

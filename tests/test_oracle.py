@@ -106,3 +106,21 @@ def test_oracle_equals_compiled_reference_random():
         a = rng.integers(0, 256, n, dtype=np.uint8)
         assert oracle.crc32_long(a) == ref.ref_crc32_long(a.ctypes.data, n)
         assert oracle.crc32_short(a) == ref.ref_crc32_short(a.ctypes.data, n)
+
+
+@pytest.mark.skipif(not oracle.ref_available(), reason="compiled reference not present (GPU box)")
+def test_compiled_reference_var_batch_mt():
+    """The reference's own crc32_long/short over a variable batch on several threads (bench.py's config-3
+    cpu_baseline leg, kind "reference") equals the oracle, including empty and <= 60-byte payloads."""
+    ref = oracle.ref_lib()
+    rng = np.random.default_rng(11)
+    lens = rng.integers(0, 5000, 3001).astype(np.uint32)
+    lens[:5] = [0, 1, 60, 61, 0]
+    offs = np.concatenate([[0], np.cumsum(lens.astype(np.uint64))[:-1]]).astype(np.uint64)
+    buf = oracle.lcg_bytes(int(lens.sum()), 19)
+    want = oracle.batch_var(buf, offs, lens)
+    for threads in (1, 3, 16):
+        out = np.zeros(lens.size, dtype=np.uint32)
+        assert ref.ref_crc32_batch_var_mt(buf.ctypes.data, offs.ctypes.data, lens.ctypes.data, lens.size,
+                                          out.ctypes.data, threads) == 0
+        assert np.array_equal(out, want), threads
