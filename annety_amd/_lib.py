@@ -54,6 +54,9 @@ SIGNATURES = [
     ("annety_lhc_verify_stream", ctypes.c_int, [_vp, _c_size, _vp, _vp, _c_size, _vp, _vp, _vp]),
     ("annety_lhc_verify_host", ctypes.c_int, [_vp, _c_size, ctypes.c_int, ctypes.c_int64, _vp, _vp, _vp, _c_size,
                                               ctypes.POINTER(_c_size), ctypes.POINTER(_c_size)]),
+    ("annety_lhc_verify_host_iov", ctypes.c_int, [_vp, _vp, _c_size, ctypes.c_int, ctypes.c_int64, _vp, _vp, _vp,
+                                                  _c_size, _vp, _vp, _vp]),
+    ("annety_pbc_verify_host_iov", ctypes.c_int, [_vp, _vp, _c_size, _vp, _vp, _vp, _c_size, _vp, _vp, _vp]),
     ("annety_pbc_parse", ctypes.c_int, [_vp, _c_size, _vp, _vp, _c_size, ctypes.POINTER(_c_size),
                                         ctypes.POINTER(_c_size)]),
     ("annety_pbc_verify_host", ctypes.c_int, [_vp, _c_size, _vp, _vp, _vp, _c_size, ctypes.POINTER(_c_size),

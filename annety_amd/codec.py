@@ -68,6 +68,34 @@ def recv_result(length_type: int, off: np.ndarray, ln: np.ndarray, used: int, in
     return DecodeResult(off, ln, used, -1 if invalid else 0, ok)
 
 
+def _iov_results(call, name, length_type, streams, max_frames):
+    """Shared body of decode_host_iov: K receive buffers through one *_verify_host_iov call; returns one
+    DecodeResult per buffer (what Codec::recv would have produced on that connection)."""
+    views = [_host_view(b) for b in streams]
+    k = len(views)
+    addrs = (ctypes.c_void_p * max(k, 1))(*[v[0] or None for v in views])
+    sizes = np.array([v[1] for v in views] or [0], dtype=np.uint64)
+    cap = sum(v[1] // (length_type + 4) + 1 for v in views) if max_frames is None else int(max_frames)
+    off = np.zeros(max(cap, 1), dtype=np.uint64)
+    ln = np.zeros(max(cap, 1), dtype=np.uint32)
+    ok = np.zeros(max(cap, 1), dtype=np.uint8)
+    nfr = np.zeros(max(k, 1), dtype=np.uint64)
+    used = np.zeros(max(k, 1), dtype=np.uint64)
+    rts = np.zeros(max(k, 1), dtype=np.int32)
+    st = call(addrs, sizes.ctypes.data, k, off.ctypes.data, ln.ctypes.data, ok.ctypes.data, cap, nfr.ctypes.data,
+              used.ctypes.data, rts.ctypes.data)
+    _lib.check(st, name)
+    out, pos = [], 0
+    for c in range(k):
+        n = int(nfr[c])
+        if rts[c] < 0:
+            _lib.check(int(rts[c]), name)
+        out.append(recv_result(length_type, off[pos:pos + n], ln[pos:pos + n], int(used[c]), rts[c] == 1,
+                               ok[pos:pos + n]))
+        pos += n
+    return out
+
+
 class LengthHeaderCodec:
     kLengthType8 = 1
     kLengthType16 = 2
@@ -158,6 +186,17 @@ class LengthHeaderCodec:
         n = k.value
         return recv_result(self.length_type, off[:n], ln[:n], int(used.value), st == 1, ok[:n])
 
+    def decode_host_iov(self, streams, max_frames: int | None = None) -> list:
+        """Codec::recv over K connections' receive buffers in one call (annety_lhc_verify_host_iov): one
+        device stream, one arena verify; returns one DecodeResult per buffer, offsets relative to it."""
+        lib = _lib.get()
+
+        def call(addrs, sizes, k, off, ln, ok, cap, nfr, used, rts):
+            return lib.annety_lhc_verify_host_iov(addrs, sizes, k, self.length_type, self.max_payload, off, ln, ok,
+                                                  cap, nfr, used, rts)
+
+        return _iov_results(call, "annety_lhc_verify_host_iov", self.length_type, streams, max_frames)
+
     # ---------------- encode ----------------
     def _encode_call(self, d_src, d_soff, d_len, n, frames, d_foff, sh):
         return _lib.get().annety_lhc_encode_batch(_dev_ptr(d_src), _dev_ptr(d_soff), _dev_ptr(d_len), n,
@@ -238,6 +277,14 @@ class ProtobufCodecFrames(LengthHeaderCodec):
             _lib.check(st, "annety_pbc_verify_host")
         n = k.value
         return recv_result(self.length_type, off[:n], ln[:n], int(used.value), st == 1, ok[:n])
+
+    def decode_host_iov(self, streams, max_frames: int | None = None) -> list:
+        lib = _lib.get()
+
+        def call(addrs, sizes, k, off, ln, ok, cap, nfr, used, rts):
+            return lib.annety_pbc_verify_host_iov(addrs, sizes, k, off, ln, ok, cap, nfr, used, rts)
+
+        return _iov_results(call, "annety_pbc_verify_host_iov", self.length_type, streams, max_frames)
 
     def plan(self, lengths: np.ndarray):
         ln = np.ascontiguousarray(lengths, dtype=np.uint32)

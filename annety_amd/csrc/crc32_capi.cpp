@@ -1237,98 +1237,247 @@ int annety_pbc_encode_batch(const void* d_src, const uint64_t* d_src_off, const 
   return encode_batch(kPbcRules, d_src, d_src_off, d_len, n, d_dst, d_frame_off, stream);
 }
 
-// Codec::recv over a host receive buffer (include/codec/Codec.h:52-76 + LengthHeaderCodec::decode :71-137):
-// the header walk runs on a helper thread while the stream is copied to the device through the pinned
-// ring (or straight from pinned caller memory); then every complete frame is verified on the device by
-// the arena path over the stream and the verdicts come back.
-static int verify_host(const FrameRules& r, const void* h_stream, size_t size, uint64_t* h_payload_off,
-                       uint32_t* h_payload_len, uint8_t* h_ok, size_t max_frames, size_t* n_frames, size_t* consumed) {
-  if (!n_frames || !consumed || !lhc_type_ok(r.T) || (!h_stream && size) ||
+// Codec::recv over K host receive buffers at once (include/codec/Codec.h:52-76 + LengthHeaderCodec::decode
+// :71-137), one per connection (src/TcpConnection.cc:438-461: each TcpConnection owns its input NetBuffer).
+// The buffers are concatenated on the device (one stream, one arena verify); on the host:
+//   * pageable buffers: the pack threads gather each ring-slot chunk of the concatenation into pinned
+//     memory, and the header walk follows right behind, reading the headers from the pinned copy the pack
+//     has just written (cache-warm) instead of from the cold source: the walk is a dependent chain of one
+//     header read per frame, which from DRAM costs ~200 ns a frame;
+//   * pinned buffers (annety_crc_host_register'ed NetBuffer arenas): DMA'd in place, walked from the source.
+// Chunk i's ring slot is reused for chunk i+2 only after its upload finished and the walk has left it.
+namespace {
+struct IovWalk {
+  const FrameRules* r;
+  const unsigned char* const* bufs;
+  const size_t* sizes;
+  const uint64_t* base;  // start of buffer c in the concatenation
+  size_t k;
+  // pack-following mode (ring != nullptr): bytes [0, packed) of the concatenation are in the ring
+  const unsigned char* const* ring = nullptr;
+  size_t chunk = 0;
+  std::atomic<uint64_t>* packed = nullptr;
+  std::atomic<uint64_t>* walked = nullptr;  // the walk needs nothing before this position any more
+  std::atomic<bool>* abort = nullptr;
+  // outputs
+  uint64_t* off;
+  uint32_t* len;
+  size_t max_frames;
+  size_t* conn_frames;
+  size_t* conn_consumed;
+  int* conn_rt;
+
+  bool wait_packed(uint64_t need) const {
+    if (!ring) return true;
+    while (packed->load(std::memory_order_acquire) < need)
+      if (abort->load(std::memory_order_relaxed)) return false;
+      else std::this_thread::yield();
+    return true;
+  }
+  unsigned char at(size_t c, uint64_t pos) const {  // byte `pos` of buffer c
+    if (!ring) return bufs[c][pos];
+    const uint64_t g = base[c] + pos;
+    return ring[(g / chunk) & 1][g % chunk];
+  }
+  void run() {
+    size_t kk = 0;
+    for (size_t c = 0; c < k; c++) {
+      const size_t T = (size_t)r->T, size = sizes[c];
+      size_t pos = 0;
+      int rc = ANNETY_CRC_OK;
+      while (kk < max_frames && size - pos >= T) {
+        if (ring) walked->store(base[c] + pos, std::memory_order_release);
+        if (!wait_packed(base[c] + pos + T)) return;
+        uint64_t u = 0;
+        for (size_t b = 0; b < T; b++) u = (u << 8) | at(c, pos + b);
+        int64_t length;  // sign-extend like peek_int8/16/32/64
+        switch (T) {
+          case 1: length = (int8_t)u; break;
+          case 2: length = (int16_t)u; break;
+          case 4: length = (int32_t)u; break;
+          default: length = (int64_t)u; break;
+        }
+        if (length < r->dec_min || (r->dec_max > 0 && length > r->dec_max)) {
+          rc = 1;  // decode returns -1: invalid length
+          break;
+        }
+        if (size - pos - T < (uint64_t)length) break;  // incomplete frame (decode returns 0)
+        if (length - 4 > 0xFFFFFFFFll) {
+          rc = ANNETY_CRC_EINVAL;  // a complete frame valid for the codec, beyond this API's 32-bit lengths
+          break;
+        }
+        off[kk] = base[c] + pos + T;  // global until the device pass is enqueued
+        len[kk] = (uint32_t)(length - 4);
+        kk++;
+        pos += T + (size_t)length;
+      }
+      conn_frames[c] = kk;  // running total; verify_host_iov turns it into this connection's count
+      conn_consumed[c] = pos;
+      conn_rt[c] = rc;
+    }
+    if (ring) walked->store(~0ull, std::memory_order_release);
+  }
+};
+}  // namespace
+
+static int verify_host_iov(const FrameRules& r, const void* const* h_bufs, const size_t* sizes, size_t k,
+                           uint64_t* h_payload_off, uint32_t* h_payload_len, uint8_t* h_ok, size_t max_frames,
+                           size_t* conn_frames, size_t* conn_consumed, int* conn_rt) {
+  if (!lhc_type_ok(r.T) || (k && (!h_bufs || !sizes || !conn_frames || !conn_consumed || !conn_rt)) ||
       (max_frames && (!h_payload_off || !h_payload_len || !h_ok)))
     return ANNETY_CRC_EINVAL;
-  *n_frames = *consumed = 0;
-  if (size == 0 || max_frames == 0)
-    return parse_frames(r, h_stream, size, h_payload_off, h_payload_len, max_frames, n_frames, consumed);
+  std::vector<uint64_t> base(k + 1, 0);
+  for (size_t c = 0; c < k; c++) {
+    if (!h_bufs[c] && sizes[c]) return ANNETY_CRC_EINVAL;
+    base[c + 1] = base[c] + sizes[c];
+    conn_frames[c] = conn_consumed[c] = 0;
+    conn_rt[c] = 0;
+  }
+  const uint64_t total = base[k];
+  IovWalk w{};
+  w.r = &r;
+  w.bufs = reinterpret_cast<const unsigned char* const*>(h_bufs);
+  w.sizes = sizes;
+  w.base = base.data();
+  w.k = k;
+  w.off = h_payload_off;
+  w.len = h_payload_len;
+  w.max_frames = max_frames;
+  w.conn_frames = conn_frames;
+  w.conn_consumed = conn_consumed;
+  w.conn_rt = conn_rt;
+  auto finish_walk = [&]() {  // per-connection counts (the walk stored running totals) and relative offsets
+    size_t prev = 0;
+    for (size_t c = 0; c < k; c++) {
+      const size_t upto = conn_frames[c];
+      for (size_t i = prev; i < upto; i++) h_payload_off[i] -= base[c];
+      conn_frames[c] = upto - prev;
+      prev = upto;
+    }
+  };
+  if (total == 0 || max_frames == 0) {
+    w.run();
+    finish_walk();
+    return ANNETY_CRC_OK;
+  }
   DeviceCtx* c = nullptr;
   int rc = stream_ctx(nullptr, &c);
   if (rc) return rc;
   std::lock_guard<std::mutex> lk(c->stg_mu);
   Staging& st = c->stg;
   if ((rc = ensure_ring(st, std::max<size_t>(st.bytes, 64u << 20), std::max<size_t>(st.outs, 1)))) return rc;
-  if (st.stream_cap < size) {
+  if (st.stream_cap < total) {
     if (st.d_stream) (void)hipFree(st.d_stream);
     st.d_stream = nullptr;
     st.stream_cap = 0;
-    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&st.d_stream), size));
-    st.stream_cap = size;
+    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&st.d_stream), total));
+    st.stream_cap = total;
   }
   hipStream_t s = st.stream[0];
-  // walk the headers while the bytes go up
-  int prc = 0;
-  std::thread walker([&] {
-    prc = parse_frames(r, h_stream, size, h_payload_off, h_payload_len, max_frames, n_frames, consumed);
-  });
+  bool pinned = true;
+  for (size_t i = 0; i < k && pinned; i++) pinned = !sizes[i] || host_pinned(h_bufs[i], sizes[i]);
+  std::atomic<uint64_t> packed{0}, walked{0};
+  std::atomic<bool> abort{false};
+  const unsigned char* ring[2] = {static_cast<const unsigned char*>(st.h_pinned[0]),
+                                  static_cast<const unsigned char*>(st.h_pinned[1])};
+  if (!pinned) {
+    w.ring = ring;
+    w.chunk = st.bytes;
+    w.packed = &packed;
+    w.walked = &walked;
+    w.abort = &abort;
+  }
+  std::thread walker([&] { w.run(); });
   auto fail = [&](int status) {
+    abort = true;
     walker.join();
     (void)hipStreamSynchronize(st.stream[0]);
     (void)hipStreamSynchronize(st.stream[1]);
     return status;
   };
-  const char* src = static_cast<const char*>(h_stream);
-  if (host_pinned(h_stream, size)) {
-    const hipError_t e = hipMemcpyAsync(st.d_stream, src, size, hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) return fail(hip_fail(e));
+  if (pinned) {
+    for (size_t i = 0; i < k; i++) {
+      if (!sizes[i]) continue;
+      const hipError_t e = hipMemcpyAsync(st.d_stream + base[i], h_bufs[i], sizes[i], hipMemcpyHostToDevice, s);
+      if (e != hipSuccess) return fail(hip_fail(e));
+    }
   } else {
-    const size_t piece = st.bytes;
-    bool busy[2] = {false, false};
-    int slot = 0;
-    for (size_t lo = 0; lo < size; lo += piece, slot ^= 1) {
-      const size_t cnt = std::min(piece, size - lo);
-      if (busy[slot]) {
+    const size_t chunk = st.bytes;
+    size_t src = 0;  // buffer holding the chunk's first byte
+    for (uint64_t lo = 0, i = 0; lo < total; lo += chunk, i++) {
+      const int slot = (int)(i & 1);
+      const uint64_t hi = std::min<uint64_t>(total, lo + chunk);
+      if (i >= 2) {  // the slot's previous chunk (i - 2): uploaded, and the walk has moved past it
         const hipError_t e = hipEventSynchronize(st.done[slot]);
         if (e != hipSuccess) return fail(hip_fail(e));
+        while (walked.load(std::memory_order_acquire) < lo - chunk) std::this_thread::yield();
       }
-      parallel_pack(static_cast<char*>(st.h_pinned[slot]), cnt, src + lo, cnt, 1, cnt);
-      hipError_t e = hipMemcpyAsync(st.d_stream + lo, st.h_pinned[slot], cnt, hipMemcpyHostToDevice, s);
+      // gather [lo, hi) of the concatenation from the buffers it spans, in parallel pieces
+      char* dst = static_cast<char*>(st.h_pinned[slot]);
+      while (src < k && base[src + 1] <= lo) src++;
+      for (size_t b = src; b < k && base[b] < hi; b++) {
+        const uint64_t a = std::max<uint64_t>(lo, base[b]), e = std::min<uint64_t>(hi, base[b + 1]);
+        if (e > a)
+          parallel_pack(dst + (a - lo), e - a, static_cast<const char*>(h_bufs[b]) + (a - base[b]), e - a, 1, e - a);
+      }
+      packed.store(hi, std::memory_order_release);  // the walk may read these headers now
+      hipError_t e = hipMemcpyAsync(st.d_stream + lo, dst, hi - lo, hipMemcpyHostToDevice, s);
       if (e == hipSuccess) e = hipEventRecord(st.done[slot], s);
       if (e != hipSuccess) return fail(hip_fail(e));
-      busy[slot] = true;
     }
   }
   walker.join();
+  const size_t nf = conn_frames[k - 1];  // running totals: the last one counts every connection's frames
+  int prc = 0;
+  for (size_t i = 0; i < k; i++)
+    if (conn_rt[i] < 0) prc = conn_rt[i];
   if (prc < 0) {
     (void)hipStreamSynchronize(s);
+    finish_walk();
     return prc;
   }
-  const size_t k = *n_frames;
-  if (k) {
-    if (st.meta_cap < k) {
+  if (nf) {
+    if (st.meta_cap < nf) {
       if (st.d_meta) (void)hipFree(st.d_meta);
       st.d_meta = nullptr;
       st.meta_cap = 0;
-      HIP_TRY(hipMalloc(reinterpret_cast<void**>(&st.d_meta), k * 17));
-      st.meta_cap = k;
+      HIP_TRY(hipMalloc(reinterpret_cast<void**>(&st.d_meta), nf * 17));
+      st.meta_cap = nf;
     }
     uint64_t* d_off = reinterpret_cast<uint64_t*>(st.d_meta);
-    uint32_t* d_len = reinterpret_cast<uint32_t*>(st.d_meta + k * 8);
-    uint32_t* d_dig = d_len + k;
-    uint8_t* d_ok = reinterpret_cast<uint8_t*>(d_dig + k);
-    hipError_t e = hipMemcpyAsync(d_off, h_payload_off, k * 8, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_len, h_payload_len, k * 4, hipMemcpyHostToDevice, s);
+    uint32_t* d_len = reinterpret_cast<uint32_t*>(st.d_meta + nf * 8);
+    uint32_t* d_dig = d_len + nf;
+    uint8_t* d_ok = reinterpret_cast<uint8_t*>(d_dig + nf);
+    hipError_t e = hipMemcpyAsync(d_off, h_payload_off, nf * 8, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipMemcpyAsync(d_len, h_payload_len, nf * 4, hipMemcpyHostToDevice, s);
     if (e != hipSuccess) {
       (void)hipStreamSynchronize(s);
+      finish_walk();
       return hip_fail(e);
     }
-    rc = run_arena(*c, st.d_stream, *consumed, d_off, d_len, k, d_dig, s, false);
+    rc = run_arena(*c, st.d_stream, total, d_off, d_len, nf, d_dig, s, false);
     if (rc == ANNETY_CRC_OK) {
-      e = launch_lhc_compare(st.d_stream, d_off, d_len, k, d_dig, d_ok, s);
-      if (e == hipSuccess) e = hipMemcpyAsync(h_ok, d_ok, k, hipMemcpyDeviceToHost, s);
+      e = launch_lhc_compare(st.d_stream, d_off, d_len, nf, d_dig, d_ok, s);
+      if (e == hipSuccess) e = hipMemcpyAsync(h_ok, d_ok, nf, hipMemcpyDeviceToHost, s);
       if (e != hipSuccess) rc = hip_fail(e);
     }
   }
-  const hipError_t e = hipStreamSynchronize(s);
+  const hipError_t e = hipStreamSynchronize(s);  // the offsets' upload has read h_payload_off by now
   if (rc == ANNETY_CRC_OK && e != hipSuccess) rc = hip_fail(e);
-  return rc ? rc : prc;
+  finish_walk();
+  return rc;
+}
+
+// One receive buffer: the K = 1 case of verify_host_iov.
+static int verify_host(const FrameRules& r, const void* h_stream, size_t size, uint64_t* h_payload_off,
+                       uint32_t* h_payload_len, uint8_t* h_ok, size_t max_frames, size_t* n_frames, size_t* consumed) {
+  if (!n_frames || !consumed || !lhc_type_ok(r.T) || (!h_stream && size) ||
+      (max_frames && (!h_payload_off || !h_payload_len || !h_ok)))
+    return ANNETY_CRC_EINVAL;
+  int crt = 0;
+  const int rc = verify_host_iov(r, &h_stream, &size, 1, h_payload_off, h_payload_len, h_ok, max_frames, n_frames,
+                                 consumed, &crt);
+  return rc ? rc : crt;
 }
 
 int annety_lhc_verify_host(const void* h_stream, size_t size, int length_type, int64_t max_payload,
@@ -1341,6 +1490,20 @@ int annety_lhc_verify_host(const void* h_stream, size_t size, int length_type, i
 int annety_pbc_verify_host(const void* h_stream, size_t size, uint64_t* h_payload_off, uint32_t* h_payload_len,
                            uint8_t* h_ok, size_t max_frames, size_t* n_frames, size_t* consumed) {
   return verify_host(kPbcRules, h_stream, size, h_payload_off, h_payload_len, h_ok, max_frames, n_frames, consumed);
+}
+
+int annety_lhc_verify_host_iov(const void* const* h_bufs, const size_t* sizes, size_t k, int length_type,
+                               int64_t max_payload, uint64_t* h_payload_off, uint32_t* h_payload_len, uint8_t* h_ok,
+                               size_t max_frames, size_t* conn_frames, size_t* conn_consumed, int* conn_rt) {
+  return verify_host_iov(lhc_rules(length_type, max_payload), h_bufs, sizes, k, h_payload_off, h_payload_len, h_ok,
+                         max_frames, conn_frames, conn_consumed, conn_rt);
+}
+
+int annety_pbc_verify_host_iov(const void* const* h_bufs, const size_t* sizes, size_t k, uint64_t* h_payload_off,
+                               uint32_t* h_payload_len, uint8_t* h_ok, size_t max_frames, size_t* conn_frames,
+                               size_t* conn_consumed, int* conn_rt) {
+  return verify_host_iov(kPbcRules, h_bufs, sizes, k, h_payload_off, h_payload_len, h_ok, max_frames, conn_frames,
+                         conn_consumed, conn_rt);
 }
 
 }  // extern "C"

@@ -81,17 +81,27 @@ class PipelinedGather:
     on the current stream, so `produce` (a kernel launch) and the gathers overlap with no extra sync."""
 
     def __init__(self, n_local: int, chunks: int, dst: int = 0, group=None, device=None, dtype=torch.int32,
-                 taper: int = 0):
+                 taper: int = 0, buffers: int = 1):
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
         self.dst, self.group = dst, group
         self.bounds = chunk_bounds(n_local, chunks, taper)
-        self.recv = (torch.empty((self.world, n_local), dtype=dtype, device=device) if self.rank == dst else None)
+        # one receive buffer per digest buffer (run_steps): gathers in flight together never share one, so
+        # the result does not depend on the backend running them in order (gloo runs them on a thread pool)
+        self.recvs = ([torch.empty((self.world, n_local), dtype=dtype, device=device) for _ in range(max(1, buffers))]
+                      if self.rank == dst else None)
+        self.last = 0  # the receive buffer of the latest step
 
-    def run(self, produce: Callable[[int, int], torch.Tensor], gather: bool = True):
+    @property
+    def recv(self) -> Optional[torch.Tensor]:
+        """On `dst`: recv[r] = rank r's digests of the latest step; None elsewhere."""
+        return self.recvs[self.last] if self.recvs is not None else None
+
+    def run(self, produce: Callable[[int, int], torch.Tensor], gather: bool = True, buf: int = 0):
         """produce(lo, hi) -> this rank's digests of payloads [lo, hi) (a view of its output). Returns
         the list of async work handles (empty when gather is False); call wait() on them."""
         handles = []
+        self.last = buf % (len(self.recvs) if self.recvs is not None else 1)
         for lo, hi in self.bounds:
             out = produce(lo, hi)
             if gather:
@@ -107,19 +117,20 @@ class PipelinedGather:
     def run_steps(self, produce: Callable[[int, int, int], torch.Tensor], steps: int, buffers: int = 2,
                   gather: bool = True) -> None:
         """`steps` consecutive steps; produce(s, lo, hi) writes step s's digests of [lo, hi) into buffer
-        s % buffers and returns that view. With two buffers, step s's handles are waited only after step
-        s+1 is launched (on a GPU: the compute stream waits for step s's gathers, no host block), so step
-        s+1 computes while step s's last gathers still read the other buffer; the buffer step s+2 reuses
-        is free by then. Everything is waited before returning."""
-        prev = []
+        s % buffers and returns that view. Step s's handles are waited (on a GPU: the compute stream waits
+        for step s's gathers, no host block) only after step s + buffers - 1 is launched, just before step
+        s + buffers reuses the buffer: with two buffers step s+1 computes while step s's last gathers still
+        read the other one. Everything is waited before returning."""
+        from collections import deque
+
+        buffers = max(1, buffers)
+        pending = deque()
         for s in range(steps):
-            h = self.run(lambda lo, hi, s=s: produce(s, lo, hi), gather=gather)
-            if buffers > 1:
-                self.wait(prev)
-                prev = h
-            else:
-                self.wait(h)
-        self.wait(prev)
+            pending.append(self.run(lambda lo, hi, s=s: produce(s, lo, hi), gather=gather, buf=s % buffers))
+            if len(pending) >= buffers:  # step s+1 reuses the buffer of step s+1-buffers
+                self.wait(pending.popleft())
+        while pending:
+            self.wait(pending.popleft())
 
 
 def digest_checksum(t: torch.Tensor) -> int:

@@ -77,6 +77,10 @@ def parse():
                    help="config 4: wait for a step's gathers before the next step starts (default: the digests "
                         "alternate between two buffers and step s+1's chunks compute while step s's last gathers "
                         "are in flight; every gather is still inside the timed region)")
+    p.add_argument("--gather-buffers", type=int, default=2,
+                   help="N>1: digest buffers the steps rotate through; step s+1 computes while step s's gather is in "
+                        "flight, and the compute stream waits for step s's gather only before step s+buffers reuses "
+                        "its buffer (1 = wait for every step's gather before the next step)")
     p.add_argument("--dist", action="store_true",
                    help="run the N>1 code path (RCCL process group, pipelined digest gather, gather check, max over "
                         "ranks) even at one rank: a one-GPU rehearsal of the multi-GPU run")
@@ -462,21 +466,24 @@ def main():
     stream = torch.cuda.current_stream(dev)
     sh = int(stream.cuda_stream)
     # strong scaling: shards differ by at most one payload; every rank gathers a buffer of the largest
-    pipe = sharded.PipelinedGather(w.n_pad, args.chunks, dst=0, device=dev, taper=args.taper) if multi else None
+    nbuf = 1 if (not multi or args.no_overlap_steps) else max(1, args.gather_buffers)
+    pipe = (sharded.PipelinedGather(w.n_pad, args.chunks, dst=0, device=dev, taper=args.taper, buffers=nbuf)
+            if multi else None)
 
     # N>1: the digests alternate between two buffers, so step s+1's chunks can be computed while step s's
     # last gathers still read the other buffer; a step's handles are waited (the compute stream waits for
     # its gathers, no host block) after the next step is launched, before the buffer comes round again
-    outs = [w.out, torch.zeros_like(w.out)] if (pipe is not None and not args.no_overlap_steps) else [w.out]
+    outs = [w.out] + [torch.zeros_like(w.out) for _ in range(nbuf - 1)]
     nstep = [0]
 
     def step(gather: bool = True):
         if pipe is None:
             w.launch(sh)
             return []
-        w.out = outs[nstep[0] % len(outs)]
+        b = nstep[0] % len(outs)
+        w.out = outs[b]
         nstep[0] += 1
-        return pipe.run(lambda lo, hi: w.launch(sh, lo, hi), gather=gather)
+        return pipe.run(lambda lo, hi: w.launch(sh, lo, hi), gather=gather, buf=b)
 
     def produce(s: int, lo: int, hi: int):
         w.out = outs[s % len(outs)]

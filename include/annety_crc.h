@@ -193,6 +193,18 @@ int annety_lhc_verify_stream(const void* d_stream, size_t stream_bytes, const ui
 int annety_lhc_verify_host(const void* h_stream, size_t size, int length_type, int64_t max_payload,
                            uint64_t* h_payload_off, uint32_t* h_payload_len, uint8_t* h_ok, size_t max_frames,
                            size_t* n_frames, size_t* consumed);
+/* Codec::recv over K connections' receive buffers in one call (one input NetBuffer per TcpConnection,
+ * src/TcpConnection.cc:438-461, each walked as include/codec/Codec.h:55-78 does): the buffers are gathered
+ * into one device stream (pinned staging; pinned buffers are DMA'd in place), each is walked exactly as
+ * annety_lhc_parse walks one, and every complete frame's CRC is verified on the device in one arena pass.
+ * Frames of connection c occupy output entries [sum(conn_frames[0..c-1]), + conn_frames[c]); their
+ * h_payload_off are relative to h_bufs[c]. conn_consumed[c] = bytes of c's complete frames; conn_rt[c] = 0
+ * (walk stopped at an incomplete frame or the end), 1 (invalid length: decode's -1, the connection is
+ * shut down) or ANNETY_CRC_EINVAL (a frame of 4 GiB or more). max_frames bounds the output arrays over all
+ * connections; connections past the bound report 0 frames. Returns 0 or a negative error. Synchronous. */
+int annety_lhc_verify_host_iov(const void* const* h_bufs, const size_t* sizes, size_t k, int length_type,
+                               int64_t max_payload, uint64_t* h_payload_off, uint32_t* h_payload_len, uint8_t* h_ok,
+                               size_t max_frames, size_t* conn_frames, size_t* conn_consumed, int* conn_rt);
 /* Host plan for a batch of LengthHeaderCodec::encode calls (:169-176): h_rt[i] (optional) = 1, or 0 for
  * an empty payload, or -1 for len > max_payload (max_payload > 0); h_frame_off[i] = where frame i starts
  * when the frames of accepted payloads are packed back to back (rejected ones take no bytes);
@@ -217,6 +229,9 @@ int annety_pbc_parse(const void* h_stream, size_t size, uint64_t* payload_off, u
                      size_t max_frames, size_t* n_frames, size_t* consumed);
 int annety_pbc_verify_host(const void* h_stream, size_t size, uint64_t* h_payload_off, uint32_t* h_payload_len,
                            uint8_t* h_ok, size_t max_frames, size_t* n_frames, size_t* consumed);
+int annety_pbc_verify_host_iov(const void* const* h_bufs, const size_t* sizes, size_t k, uint64_t* h_payload_off,
+                               uint32_t* h_payload_len, uint8_t* h_ok, size_t max_frames, size_t* conn_frames,
+                               size_t* conn_consumed, int* conn_rt);
 int annety_pbc_encode_plan(const uint32_t* h_len, size_t n, uint64_t* h_frame_off, int8_t* h_rt, uint64_t* total);
 int annety_pbc_encode_batch(const void* d_src, const uint64_t* d_src_off, const uint32_t* d_len, size_t n,
                             void* d_dst, const uint64_t* d_frame_off, void* stream);

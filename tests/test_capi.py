@@ -219,3 +219,54 @@ def test_boundary_error_paths_without_device():
         # valid arguments, no device: a negative status (no HIP device), never a crash
         assert lib.annety_crc32_batch_fixed(ctypes.addressof(buf), 4, 16, 16, ctypes.addressof(out), None) < 0
         assert lib.annety_crc_stream_release(None) < 0
+
+
+def test_product_kernels_do_not_spill(tmp_path):
+    """Every gfx950 kernel in libannety_crc.so runs without scratch (no VGPR spills): the 1024-lane stitch
+    variant that returned wrong digests in round 2 was the only build that spilled (DESIGN.md §7.2;
+    microbench/isa_check.py), so a change that pushes a product kernel into spilling fails here, on the
+    CPU, before it reaches a GPU."""
+    import shutil
+
+    objdump = "/opt/rocm/lib/llvm/bin/llvm-objdump"
+    readelf = "/opt/rocm/lib/llvm/bin/llvm-readelf"
+    if not (os.path.exists(objdump) and os.path.exists(readelf)):
+        pytest.skip("ROCm llvm tools not present")
+    lib = tmp_path / "lib.so"
+    shutil.copy(_lib.lib_path(), lib)
+    subprocess.run([objdump, "--offloading", str(lib)], check=True, capture_output=True, cwd=tmp_path)
+    objs = sorted(p for p in tmp_path.iterdir() if "gfx950" in p.name)
+    assert objs, "no gfx950 code object in the library"
+    kernels = {}
+    for co in objs:
+        notes = subprocess.run([readelf, "--notes", str(co)], check=True, capture_output=True, text=True).stdout
+        for block in notes.split("  - .agpr_count")[1:]:
+            name = re.search(r"\.name:\s+(\S+)", block).group(1)
+            kernels[name] = int(re.search(r"\.private_segment_fixed_size:\s+(\d+)", block).group(1))
+    assert any("crc32_arena_stitch_kernel" in k for k in kernels) and any("oneround" in k for k in kernels)
+    spilling = {k: v for k, v in kernels.items() if v}
+    assert not spilling, spilling
+
+
+def test_verify_host_iov_arguments_without_device():
+    """annety_lhc_verify_host_iov argument rules (before any device work): bad length type, a NULL buffer
+    with a size, missing outputs; an all-empty call walks nothing and needs no device."""
+    import ctypes
+
+    lib = _lib.get()
+    sizes = (ctypes.c_size_t * 2)(0, 0)
+    bufs = (ctypes.c_void_p * 2)(None, None)
+    nf = (ctypes.c_size_t * 2)(9, 9)
+    used = (ctypes.c_size_t * 2)(9, 9)
+    rt = (ctypes.c_int * 2)(9, 9)
+    assert lib.annety_lhc_verify_host_iov(bufs, sizes, 2, 3, 0, None, None, None, 0, nf, used, rt) == -1
+    assert lib.annety_lhc_verify_host_iov(bufs, sizes, 2, 4, 0, None, None, None, 0, nf, used, rt) == 0
+    assert list(nf) == [0, 0] and list(used) == [0, 0] and list(rt) == [0, 0]
+    sizes[1] = 10
+    assert lib.annety_lhc_verify_host_iov(bufs, sizes, 2, 4, 0, None, None, None, 0, nf, used, rt) == -1
+    assert lib.annety_lhc_verify_host_iov(bufs, sizes, 2, 4, 0, None, None, None, 5, nf, used, rt) == -1
+    # the host walk alone (max_frames 0: no device): one buffer with an invalid length reports rt 1
+    hdr = (ctypes.c_uint8 * 4)(0, 0, 0, 2)  # length 2 < 4
+    bufs[0], sizes[0], sizes[1] = ctypes.addressof(hdr), 4, 0
+    assert lib.annety_lhc_verify_host_iov(bufs, sizes, 2, 4, 0, None, None, None, 0, nf, used, rt) == 0
+    assert list(nf) == [0, 0] and list(used) == [0, 0] and list(rt) == [0, 0]  # max_frames 0: nothing walked

@@ -142,7 +142,7 @@ def _steps_worker(rank, world, port, n_local, L, chunks, steps, buffers, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         outs = [torch.zeros(n_local, dtype=torch.int32) for _ in range(buffers)]
-        pipe = sharded.PipelinedGather(n_local, chunks, dst=0)
+        pipe = sharded.PipelinedGather(n_local, chunks, dst=0, buffers=buffers)
 
         def produce(s, lo, hi):
             arena = oracle.lcg_bytes(n_local * L, 100 * s + rank)
@@ -162,7 +162,7 @@ def _steps_worker(rank, world, port, n_local, L, chunks, steps, buffers, q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("buffers", [1, 2])
+@pytest.mark.parametrize("buffers", [1, 2, 3])
 def test_gloo_world2_run_steps(buffers):
     n_local, L, chunks, steps = 600, 128, 3, 5
     ctx = mp.get_context("spawn")

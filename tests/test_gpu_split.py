@@ -22,7 +22,7 @@ class _split:
     """The split policy (annety_crc_set_split) for the duration of a block; back to auto after."""
 
     def __init__(self, mode: str):
-        self.mode = int(mode)
+        self.mode = int(mode) if mode != "" else -1  # "" = auto
 
     def __enter__(self):
         import annety_amd

@@ -400,3 +400,70 @@ def test_property_plan_equals_sequential_encode(lens, T, maxp):
         assert int(rt[i]) == r and int(off[i]) == pos
         pos += len(out)
     assert total == pos
+
+
+@pytest.mark.gpu
+def test_gpu_decode_host_iov_replays_every_recorded_stream(golden, gpu):
+    """annety_lhc_verify_host_iov: the reference codec's 95 recorded decode streams as 95 connections'
+    receive buffers, one call per codec configuration (T, max_payload) - all 95 in as many calls as there
+    are configurations, 93 of them in the four largest calls - each connection's frames, consumed bytes
+    and rt equal to the reference's Codec::recv sequence. Then the same with the buffers pinned."""
+    import annety_amd
+
+    groups = {}
+    for c in golden("lhc.json")["decode"]:
+        groups.setdefault((c["T"], c["max_payload"]), []).append(c)
+    assert sum(len(v) for v in groups.values()) == 95
+    for (T, mp), cases in groups.items():
+        codec = LengthHeaderCodec(T, True, mp)
+        bufs = [bytes.fromhex(c["stream"]) for c in cases]
+        res = codec.decode_host_iov(bufs)
+        assert len(res) == len(cases)
+        for c, r in zip(cases, res):
+            assert [[int(o), int(n)] for o, n in zip(r.payload_off, r.payload_len)] == c["frames"], c["name"]
+            assert (r.consumed, r.rt) == (c["consumed"], c["rt"]), c["name"]
+        pinned = []
+        for b in bufs:
+            p = annety_amd.PinnedHostBuffer(max(1, len(b)))
+            p.array[: len(b)] = np.frombuffer(b, dtype=np.uint8)
+            pinned.append(p)
+        res2 = codec.decode_host_iov([p.array[: len(b)] for p, b in zip(pinned, bufs)])
+        for c, r in zip(cases, res2):
+            assert [[int(o), int(n)] for o, n in zip(r.payload_off, r.payload_len)] == c["frames"], c["name"]
+            assert (r.consumed, r.rt) == (c["consumed"], c["rt"]), c["name"]
+        for p in pinned:
+            p.close()
+
+
+@pytest.mark.gpu
+def test_gpu_decode_host_iov_large(gpu):
+    """Many connections whose buffers cross the 64 MiB staging chunks (frames and headers straddle chunk
+    boundaries, the walk follows the pack), with corrupted frames and ragged tails: every connection's
+    verdicts equal the single-stream path's and the oracle's."""
+    rng = np.random.default_rng(21)
+    codec = LengthHeaderCodec(4)
+    bufs, want = [], []
+    for conn in range(40):
+        n = int(rng.integers(0, 900))
+        lens = np.minimum(65536, 64 * rng.zipf(1.3, n) + rng.integers(0, 64, n)).astype(np.int64) if n else []
+        body = oracle.lcg_bytes(int(np.sum(lens)) if n else 0, 500 + conn)
+        out, pos, starts = [], 0, []
+        for L in (lens.tolist() if n else []):
+            starts.append(sum(len(x) for x in out))
+            out.append(oracle.lhc_encode(body[pos:pos + L], 4)[1])
+            pos += L
+        s = bytearray(b"".join(out))
+        if n and conn % 3 == 0:  # a corrupted frame
+            b = int(rng.integers(0, n))
+            s[starts[b] + 4] ^= 1
+        s += bytes(int(rng.integers(0, 30)))  # ragged tail: an incomplete next frame
+        bufs.append(bytes(s))
+        want.append(codec.decode_host(bytes(s)))
+    assert sum(len(b) for b in bufs) > 150 << 20  # several staging chunks
+    got = codec.decode_host_iov(bufs)
+    for w, g in zip(want, got):
+        assert np.array_equal(w.payload_off, g.payload_off) and np.array_equal(w.payload_len, g.payload_len)
+        assert (w.consumed, w.rt) == (g.consumed, g.rt) and np.array_equal(w.ok, g.ok)
+    # a frame cap smaller than the total: later connections report no frames
+    capped = codec.decode_host_iov(bufs, max_frames=100)
+    assert sum(int(r.ok.size) for r in capped) == 100
