@@ -435,6 +435,9 @@ int stream_ctx(hipStream_t stream, DeviceCtx** out) {
   return ANNETY_CRC_OK;
 }
 
+// The current device's context (microbench harnesses, which include this file).
+[[maybe_unused]] int current_ctx(DeviceCtx** out) { return stream_ctx(nullptr, out); }
+
 const void* group_image(const DeviceCtx& c, uint32_t g) {
   return static_cast<const char*>(c.d_groups) + (size_t)group_index(g) * kGroupImageBytes;
 }
@@ -1239,85 +1242,47 @@ int annety_pbc_encode_batch(const void* d_src, const uint64_t* d_src_off, const 
 
 // Codec::recv over K host receive buffers at once (include/codec/Codec.h:52-76 + LengthHeaderCodec::decode
 // :71-137), one per connection (src/TcpConnection.cc:438-461: each TcpConnection owns its input NetBuffer).
-// The buffers are concatenated on the device (one stream, one arena verify); on the host:
-//   * pageable buffers: the pack threads gather each ring-slot chunk of the concatenation into pinned
-//     memory, and the header walk follows right behind, reading the headers from the pinned copy the pack
-//     has just written (cache-warm) instead of from the cold source: the walk is a dependent chain of one
-//     header read per frame, which from DRAM costs ~200 ns a frame;
-//   * pinned buffers (annety_crc_host_register'ed NetBuffer arenas): DMA'd in place, walked from the source.
-// Chunk i's ring slot is reused for chunk i+2 only after its upload finished and the walk has left it.
+// The buffers are concatenated on the device (one stream, one arena verify). On the host each buffer's
+// header walk - a dependent chain of one header read per frame, ~140-170 ns a frame from DRAM - runs on
+// its own walker thread (connections are independent), while the buffers are packed into pinned memory
+// and uploaded (pinned buffers, e.g. annety_crc_host_register'ed NetBuffer arenas, are DMA'd in place).
 namespace {
-struct IovWalk {
-  const FrameRules* r;
-  const unsigned char* const* bufs;
-  const size_t* sizes;
-  const uint64_t* base;  // start of buffer c in the concatenation
-  size_t k;
-  // pack-following mode (ring != nullptr): bytes [0, packed) of the concatenation are in the ring
-  const unsigned char* const* ring = nullptr;
-  size_t chunk = 0;
-  std::atomic<uint64_t>* packed = nullptr;
-  std::atomic<uint64_t>* walked = nullptr;  // the walk needs nothing before this position any more
-  std::atomic<bool>* abort = nullptr;
-  // outputs
-  uint64_t* off;
-  uint32_t* len;
-  size_t max_frames;
-  size_t* conn_frames;
-  size_t* conn_consumed;
-  int* conn_rt;
-
-  bool wait_packed(uint64_t need) const {
-    if (!ring) return true;
-    while (packed->load(std::memory_order_acquire) < need)
-      if (abort->load(std::memory_order_relaxed)) return false;
-      else std::this_thread::yield();
-    return true;
-  }
-  unsigned char at(size_t c, uint64_t pos) const {  // byte `pos` of buffer c
-    if (!ring) return bufs[c][pos];
-    const uint64_t g = base[c] + pos;
-    return ring[(g / chunk) & 1][g % chunk];
-  }
-  void run() {
-    size_t kk = 0;
-    for (size_t c = 0; c < k; c++) {
-      const size_t T = (size_t)r->T, size = sizes[c];
-      size_t pos = 0;
-      int rc = ANNETY_CRC_OK;
-      while (kk < max_frames && size - pos >= T) {
-        if (ring) walked->store(base[c] + pos, std::memory_order_release);
-        if (!wait_packed(base[c] + pos + T)) return;
-        uint64_t u = 0;
-        for (size_t b = 0; b < T; b++) u = (u << 8) | at(c, pos + b);
-        int64_t length;  // sign-extend like peek_int8/16/32/64
-        switch (T) {
-          case 1: length = (int8_t)u; break;
-          case 2: length = (int16_t)u; break;
-          case 4: length = (int32_t)u; break;
-          default: length = (int64_t)u; break;
-        }
-        if (length < r->dec_min || (r->dec_max > 0 && length > r->dec_max)) {
-          rc = 1;  // decode returns -1: invalid length
-          break;
-        }
-        if (size - pos - T < (uint64_t)length) break;  // incomplete frame (decode returns 0)
-        if (length - 4 > 0xFFFFFFFFll) {
-          rc = ANNETY_CRC_EINVAL;  // a complete frame valid for the codec, beyond this API's 32-bit lengths
-          break;
-        }
-        off[kk] = base[c] + pos + T;  // global until the device pass is enqueued
-        len[kk] = (uint32_t)(length - 4);
-        kk++;
-        pos += T + (size_t)length;
-      }
-      conn_frames[c] = kk;  // running total; verify_host_iov turns it into this connection's count
-      conn_consumed[c] = pos;
-      conn_rt[c] = rc;
-    }
-    if (ring) walked->store(~0ull, std::memory_order_release);
-  }
+struct ConnWalk {
+  std::vector<uint64_t> off;  // relative to the connection's buffer
+  std::vector<uint32_t> len;
+  size_t consumed = 0;
+  int rt = 0;
 };
+
+// LengthHeaderCodec::decode's framing over one buffer, at most `cap` frames (parse_frames' rules).
+void walk_conn(const FrameRules& r, const unsigned char* p, size_t size, size_t cap, ConnWalk& w) {
+  const size_t T = (size_t)r.T;
+  size_t pos = 0;
+  while (w.off.size() < cap && size - pos >= T) {
+    uint64_t u = 0;
+    for (size_t b = 0; b < T; b++) u = (u << 8) | p[pos + b];
+    int64_t length;  // sign-extend like peek_int8/16/32/64
+    switch (T) {
+      case 1: length = (int8_t)u; break;
+      case 2: length = (int16_t)u; break;
+      case 4: length = (int32_t)u; break;
+      default: length = (int64_t)u; break;
+    }
+    if (length < r.dec_min || (r.dec_max > 0 && length > r.dec_max)) {
+      w.rt = 1;  // decode returns -1: invalid length
+      break;
+    }
+    if (size - pos - T < (uint64_t)length) break;  // incomplete frame (decode returns 0)
+    if (length - 4 > 0xFFFFFFFFll) {
+      w.rt = ANNETY_CRC_EINVAL;  // a complete frame valid for the codec, beyond this API's 32-bit lengths
+      break;
+    }
+    w.off.push_back(pos + T);
+    w.len.push_back((uint32_t)(length - 4));
+    pos += T + (size_t)length;
+  }
+  w.consumed = pos;
+}
 }  // namespace
 
 static int verify_host_iov(const FrameRules& r, const void* const* h_bufs, const size_t* sizes, size_t k,
@@ -1334,67 +1299,47 @@ static int verify_host_iov(const FrameRules& r, const void* const* h_bufs, const
     conn_rt[c] = 0;
   }
   const uint64_t total = base[k];
-  IovWalk w{};
-  w.r = &r;
-  w.bufs = reinterpret_cast<const unsigned char* const*>(h_bufs);
-  w.sizes = sizes;
-  w.base = base.data();
-  w.k = k;
-  w.off = h_payload_off;
-  w.len = h_payload_len;
-  w.max_frames = max_frames;
-  w.conn_frames = conn_frames;
-  w.conn_consumed = conn_consumed;
-  w.conn_rt = conn_rt;
-  auto finish_walk = [&]() {  // per-connection counts (the walk stored running totals) and relative offsets
-    size_t prev = 0;
-    for (size_t c = 0; c < k; c++) {
-      const size_t upto = conn_frames[c];
-      for (size_t i = prev; i < upto; i++) h_payload_off[i] -= base[c];
-      conn_frames[c] = upto - prev;
-      prev = upto;
-    }
+  if (total == 0 || max_frames == 0) return ANNETY_CRC_OK;
+  // the walks: connections are independent, one walker thread per connection up to a pool's worth
+  std::vector<ConnWalk> walks(k);
+  std::atomic<size_t> next{0};
+  auto walker = [&] {
+    for (size_t c; (c = next.fetch_add(1)) < k;)
+      walk_conn(r, static_cast<const unsigned char*>(h_bufs[c]), sizes[c], max_frames, walks[c]);
   };
-  if (total == 0 || max_frames == 0) {
-    w.run();
-    finish_walk();
-    return ANNETY_CRC_OK;
-  }
+  const size_t nwalk = std::min<size_t>(k, std::max<size_t>(1, std::min(8u, std::thread::hardware_concurrency())));
+  std::vector<std::thread> walkers;
+  for (size_t i = 0; i < nwalk; i++) walkers.emplace_back(walker);
+  auto join_walkers = [&] {
+    for (auto& t : walkers)
+      if (t.joinable()) t.join();
+  };
   DeviceCtx* c = nullptr;
   int rc = stream_ctx(nullptr, &c);
-  if (rc) return rc;
-  std::lock_guard<std::mutex> lk(c->stg_mu);
+  if (rc) {
+    join_walkers();
+    return rc;
+  }
+  std::unique_lock<std::mutex> lk(c->stg_mu);
   Staging& st = c->stg;
-  if ((rc = ensure_ring(st, std::max<size_t>(st.bytes, 64u << 20), std::max<size_t>(st.outs, 1)))) return rc;
+  auto fail = [&](int status) {
+    join_walkers();
+    if (st.stream[0]) (void)hipStreamSynchronize(st.stream[0]);
+    if (st.stream[1]) (void)hipStreamSynchronize(st.stream[1]);
+    return status;
+  };
+  if ((rc = ensure_ring(st, std::max<size_t>(st.bytes, 64u << 20), std::max<size_t>(st.outs, 1)))) return fail(rc);
   if (st.stream_cap < total) {
     if (st.d_stream) (void)hipFree(st.d_stream);
     st.d_stream = nullptr;
     st.stream_cap = 0;
-    HIP_TRY(hipMalloc(reinterpret_cast<void**>(&st.d_stream), total));
+    const hipError_t e = hipMalloc(reinterpret_cast<void**>(&st.d_stream), total);
+    if (e != hipSuccess) return fail(hip_fail(e));
     st.stream_cap = total;
   }
   hipStream_t s = st.stream[0];
   bool pinned = true;
   for (size_t i = 0; i < k && pinned; i++) pinned = !sizes[i] || host_pinned(h_bufs[i], sizes[i]);
-  std::atomic<uint64_t> packed{0}, walked{0};
-  std::atomic<bool> abort{false};
-  const unsigned char* ring[2] = {static_cast<const unsigned char*>(st.h_pinned[0]),
-                                  static_cast<const unsigned char*>(st.h_pinned[1])};
-  if (!pinned) {
-    w.ring = ring;
-    w.chunk = st.bytes;
-    w.packed = &packed;
-    w.walked = &walked;
-    w.abort = &abort;
-  }
-  std::thread walker([&] { w.run(); });
-  auto fail = [&](int status) {
-    abort = true;
-    walker.join();
-    (void)hipStreamSynchronize(st.stream[0]);
-    (void)hipStreamSynchronize(st.stream[1]);
-    return status;
-  };
   if (pinned) {
     for (size_t i = 0; i < k; i++) {
       if (!sizes[i]) continue;
@@ -1407,10 +1352,9 @@ static int verify_host_iov(const FrameRules& r, const void* const* h_bufs, const
     for (uint64_t lo = 0, i = 0; lo < total; lo += chunk, i++) {
       const int slot = (int)(i & 1);
       const uint64_t hi = std::min<uint64_t>(total, lo + chunk);
-      if (i >= 2) {  // the slot's previous chunk (i - 2): uploaded, and the walk has moved past it
+      if (i >= 2) {  // the slot's previous upload has finished reading it
         const hipError_t e = hipEventSynchronize(st.done[slot]);
         if (e != hipSuccess) return fail(hip_fail(e));
-        while (walked.load(std::memory_order_acquire) < lo - chunk) std::this_thread::yield();
       }
       // gather [lo, hi) of the concatenation from the buffers it spans, in parallel pieces
       char* dst = static_cast<char*>(st.h_pinned[slot]);
@@ -1420,20 +1364,36 @@ static int verify_host_iov(const FrameRules& r, const void* const* h_bufs, const
         if (e > a)
           parallel_pack(dst + (a - lo), e - a, static_cast<const char*>(h_bufs[b]) + (a - base[b]), e - a, 1, e - a);
       }
-      packed.store(hi, std::memory_order_release);  // the walk may read these headers now
       hipError_t e = hipMemcpyAsync(st.d_stream + lo, dst, hi - lo, hipMemcpyHostToDevice, s);
       if (e == hipSuccess) e = hipEventRecord(st.done[slot], s);
       if (e != hipSuccess) return fail(hip_fail(e));
     }
   }
-  walker.join();
-  const size_t nf = conn_frames[k - 1];  // running totals: the last one counts every connection's frames
+  join_walkers();
+  // frames in connection order, the output bound applied in that order (Codec::recv's per-connection
+  // results; a connection cut by the bound stops as annety_lhc_parse does at max_frames: rt 0)
+  size_t nf = 0;
   int prc = 0;
-  for (size_t i = 0; i < k; i++)
-    if (conn_rt[i] < 0) prc = conn_rt[i];
+  for (size_t i = 0; i < k; i++) {
+    ConnWalk& w = walks[i];
+    size_t m = w.off.size();
+    if (nf + m > max_frames) {
+      m = max_frames - nf;
+      w.rt = 0;
+      w.consumed = m ? w.off[m - 1] + w.len[m - 1] + 4 : 0;
+    }
+    for (size_t f = 0; f < m; f++) {
+      h_payload_off[nf + f] = w.off[f];
+      h_payload_len[nf + f] = w.len[f];
+    }
+    conn_frames[i] = m;
+    conn_consumed[i] = w.consumed;
+    conn_rt[i] = w.rt;
+    if (w.rt < 0) prc = w.rt;
+    nf += m;
+  }
   if (prc < 0) {
     (void)hipStreamSynchronize(s);
-    finish_walk();
     return prc;
   }
   if (nf) {
@@ -1441,20 +1401,21 @@ static int verify_host_iov(const FrameRules& r, const void* const* h_bufs, const
       if (st.d_meta) (void)hipFree(st.d_meta);
       st.d_meta = nullptr;
       st.meta_cap = 0;
-      HIP_TRY(hipMalloc(reinterpret_cast<void**>(&st.d_meta), nf * 17));
+      const hipError_t e = hipMalloc(reinterpret_cast<void**>(&st.d_meta), nf * 17);
+      if (e != hipSuccess) return fail(hip_fail(e));
       st.meta_cap = nf;
     }
+    // device offsets are into the concatenation; the host outputs stay relative to each buffer
+    std::vector<uint64_t> goff(nf);
+    for (size_t i = 0, f = 0; i < k; i++)
+      for (size_t q = 0; q < conn_frames[i]; q++, f++) goff[f] = h_payload_off[f] + base[i];
     uint64_t* d_off = reinterpret_cast<uint64_t*>(st.d_meta);
     uint32_t* d_len = reinterpret_cast<uint32_t*>(st.d_meta + nf * 8);
     uint32_t* d_dig = d_len + nf;
     uint8_t* d_ok = reinterpret_cast<uint8_t*>(d_dig + nf);
-    hipError_t e = hipMemcpyAsync(d_off, h_payload_off, nf * 8, hipMemcpyHostToDevice, s);
+    hipError_t e = hipMemcpyAsync(d_off, goff.data(), nf * 8, hipMemcpyHostToDevice, s);
     if (e == hipSuccess) e = hipMemcpyAsync(d_len, h_payload_len, nf * 4, hipMemcpyHostToDevice, s);
-    if (e != hipSuccess) {
-      (void)hipStreamSynchronize(s);
-      finish_walk();
-      return hip_fail(e);
-    }
+    if (e != hipSuccess) return fail(hip_fail(e));
     rc = run_arena(*c, st.d_stream, total, d_off, d_len, nf, d_dig, s, false);
     if (rc == ANNETY_CRC_OK) {
       e = launch_lhc_compare(st.d_stream, d_off, d_len, nf, d_dig, d_ok, s);
@@ -1462,9 +1423,8 @@ static int verify_host_iov(const FrameRules& r, const void* const* h_bufs, const
       if (e != hipSuccess) rc = hip_fail(e);
     }
   }
-  const hipError_t e = hipStreamSynchronize(s);  // the offsets' upload has read h_payload_off by now
+  const hipError_t e = hipStreamSynchronize(s);  // also: the offsets' upload has read goff
   if (rc == ANNETY_CRC_OK && e != hipSuccess) rc = hip_fail(e);
-  finish_walk();
   return rc;
 }
 
