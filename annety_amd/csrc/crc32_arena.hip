@@ -145,7 +145,6 @@ struct StitchGeo {
   size_t n;
   uint64_t zero_line;
   uint32_t* out;
-  bool linear;  // S of full superblocks at S[block * 8 + line] (store-wave line pass), else burst layout
 };
 
 // One payload's loads and the plan that consumes them. Steps 0..3 = head block, first partial
@@ -185,13 +184,8 @@ struct Stitcher {
     const uint64_t sb = g.sb0 + (rb >> 3);
     const bool edge = sb < g.fs0 || sb >= g.fs1;
     const uint32_t r = (uint32_t)(rb - (g.fs0 - g.sb0) * 8);  // block of the full range (< 2^32: host check)
-    uint64_t full;
-    if (g.linear) {
-      full = ((uint64_t)r * 8 + a) * 4;
-    } else {
-      const uint32_t t = (r >> 6) / g.L;  // task; lane group = r - t * 64 L
-      full = arena_s_word(t, r - t * 64 * g.L, a, g.W) * 4;
-    }
+    const uint32_t t = (r >> 6) / g.L;                        // task; lane group = r - t * 64 L
+    const uint64_t full = arena_s_word(t, r - t * 64 * g.L, a, g.W) * 4;
     const uint64_t ed = ((sb == g.sb0 ? 0 : 64) + (rb & 7) * 8 + a) * 4;
     return edge ? (uint64_t)(uintptr_t)g.S_edge + ed : (uint64_t)(uintptr_t)g.S + full;
   }
@@ -487,15 +481,6 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(WPE))) void
   }
 }
 
-// First launch, store-wave form (crc32_arena_lines.h arena_line_pass_sw): 8 streaming waves + 1 store wave.
-__global__ __launch_bounds__(kSwBlock) void crc32_arena_lines_sw_kernel(const uint8_t* __restrict__ base, LineOut ar,
-                                                                        const uint4* __restrict__ img_slice,
-                                                                        const uint4* __restrict__ img_group8,
-                                                                        const uint4* __restrict__ img_sb) {
-  __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsArenaSwBytes / 16];
-  arena_line_pass_sw(base, ar, blockIdx.x, gridDim.x, lds4, img_slice, img_group8, img_sb);
-}
-
 // First launch: the line pass.
 template <int PROBE = 0>
 __global__ __launch_bounds__(kBlock) void crc32_arena_lines_kernel(const uint8_t* __restrict__ base, LineOut ar,
@@ -531,15 +516,6 @@ size_t stitch_blocks(const ArenaLaunch& a) {
   return std::max<size_t>(1, std::min<size_t>(a.max_blocks, (a.n + kStitchBlock - 1) / kStitchBlock));
 }
 
-// The line pass with a store wave (S linear) or with S bursts from the streaming waves; read once.
-bool line_store_wave() {
-  static const bool sw = [] {
-    const char* e = std::getenv("ANNETY_CRC_LINE_SW");
-    return e && e[0] == '1';
-  }();
-  return sw;
-}
-
 StitchGeo stitch_geo(const ArenaLaunch& a, const ArenaGeom& geo) {
   StitchGeo s;
   s.base = static_cast<const uint8_t*>(a.base);
@@ -561,7 +537,6 @@ StitchGeo stitch_geo(const ArenaLaunch& a, const ArenaGeom& geo) {
   s.n = a.n;
   s.zero_line = (uint64_t)(uintptr_t)a.zero_line;
   s.out = a.out;
-  s.linear = line_store_wave();
   return s;
 }
 
@@ -603,18 +578,7 @@ hipError_t launch_arena_lines_p(const ArenaLaunch& a, hipStream_t stream) {
   return hipGetLastError();
 }
 
-hipError_t launch_arena_lines_sw(const ArenaLaunch& a, hipStream_t stream) {
-  const ArenaGeom geo = arena_geom(a);
-  hipLaunchKernelGGL(crc32_arena_lines_sw_kernel, dim3((unsigned)geo.blocks), dim3(kSwBlock), 0, stream,
-                     reinterpret_cast<const uint8_t*>((uintptr_t)(a.fs0 * 8192)), line_out(a, geo),
-                     static_cast<const uint4*>(a.img_slice), static_cast<const uint4*>(a.img_group8),
-                     static_cast<const uint4*>(a.img_sb));
-  return hipGetLastError();
-}
-
-hipError_t launch_arena_lines(const ArenaLaunch& a, hipStream_t stream) {
-  return line_store_wave() ? launch_arena_lines_sw(a, stream) : launch_arena_lines_p<0>(a, stream);
-}
+hipError_t launch_arena_lines(const ArenaLaunch& a, hipStream_t stream) { return launch_arena_lines_p<0>(a, stream); }
 
 hipError_t launch_arena(const ArenaLaunch& a, hipStream_t stream) {
   if (a.nsb) {

@@ -4,6 +4,7 @@
 #include "../annety_amd/csrc/crc32_arena.hip"
 #include "../annety_amd/csrc/crc32_frames.hip"
 #include "../annety_amd/csrc/crc32_capi.cpp"
+#include "arena_sw.h"
 #include <cstdio>
 #include <string>
 
@@ -74,6 +75,10 @@ int main(int argc, char** argv) {
   t([&] { lines<1>(*c, a); }, "  no S store");
   t([&] { lines<2>(*c, a); }, "  no superblock scan");
   t([&] { lines<3>(*c, a); }, "  no S store, no superblock scan");
+  t([&] { CK(launch_arena_lines_sw<0>(a, 0)); }, "store wave (8 + 1 waves, LDS ring)");
+  t([&] { CK(launch_arena_lines_sw<1>(a, 0)); }, "  ring, store wave stores nothing");
+  t([&] { CK(launch_arena_lines_sw<2>(a, 0)); }, "  no ring (9 waves, no hand-off)");
+  t([&] { lines<0>(*c, a); }, "arena lines (product) again");
   // S traffic alone: the same 32 MiB of stores as a separate pass
   t([&] { CK(hipMemsetAsync(a.scratch, 0, a.nsb * 64 * 4, 0)); }, "memset of S (32 MiB)");
   return 0;

@@ -1,7 +1,7 @@
 #!/bin/bash
-# Store-wave line pass (ANNETY_CRC_LINE_SW=1) on the GPU box: correctness on the arena tests first (a short
-# time limit per step: a hang in the LDS hand-off would show here), then config-3 bench lines alternating
-# with the burst line pass. Run from the repo root.
+# Round-3 A/B of the store-wave arena line pass (then selected by ANNETY_CRC_LINE_SW=1; now rejected and
+# moved to microbench/arena_sw.h): arena tests under it, then config-3 bench lines alternating
+# with the burst line pass. Kept as the record of how profiles/r03/store_wave/ was produced.
 set -e
 O=$GRAFT_REPO_ROOT/gpurun_out/${1:-r03_sw}
 mkdir -p $O
