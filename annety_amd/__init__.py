@@ -29,6 +29,7 @@ from .crc32c import (  # noqa: F401
     scratch_stats,
     set_split,
     stream_release,
+    var_path_stats,
     tables,
 )
 from ._lib import CrcError, lib_path  # noqa: F401
@@ -49,6 +50,7 @@ __all__ = [
     "scratch_stats",
     "set_split",
     "stream_release",
+    "var_path_stats",
     "tables",
     "LengthHeaderCodec",
     "ProtobufCodecFrames",

@@ -97,6 +97,16 @@ def scratch_stats(device: int = 0) -> dict:
     return {"slots": v[0].value, "handoffs": v[1].value, "device_syncs": v[2].value}
 
 
+def var_path_stats(device: int = 0) -> dict:
+    """annety_crc_var_path_stats: how many automatic variable-batch calls took the arena / sorted path."""
+    import ctypes
+
+    a, b = ctypes.c_uint64(), ctypes.c_uint64()
+    _lib.check(_lib.get().annety_crc_var_path_stats(int(device), ctypes.byref(a), ctypes.byref(b)),
+               "annety_crc_var_path_stats")
+    return {"arena": a.value, "sorted": b.value}
+
+
 def stream_release(stream) -> None:
     """annety_crc_stream_release: drop a stream's scratch (stream-ordered) before the stream is destroyed."""
     h = stream if isinstance(stream, int) else int(stream.cuda_stream)

@@ -145,6 +145,8 @@ struct StitchGeo {
   size_t n;
   uint64_t zero_line;
   uint32_t* out;
+  const uint64_t* check;  // ArenaLaunch::check
+  uint64_t check_lo, check_hi;
 };
 
 // One payload's loads and the plan that consumes them. Steps 0..3 = head block, first partial
@@ -382,9 +384,11 @@ __device__ __forceinline__ LaneCtx lane_ctx() {
 //   PIPE (microbench A/B, product = 0): 1 = the next payload's loads are issued before the
 //   current one is folded; 2 = a lane's first two payloads' descriptors and plan loads issued together.
 template <bool UPD, int BLK = kStitchBlock, int PROBE = 0, int PIPE = 0>
-__global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchGeo g, const uint4* __restrict__ img_slice,
+__global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchGeo g0, const uint4* __restrict__ img_slice,
                                                                  const uint4* __restrict__ img_stitch) {
   __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsStitchImageBytes / 16];
+  StitchGeo g = g0;
+  if (!extent_matches(g.check, g.check_lo, g.check_hi)) g.byte_lo = g.byte_hi = 0;  // the line pass did nothing
   const Stitcher<UPD, PROBE> st{g, reinterpret_cast<const uint32_t*>(lds4), lane_ctx()};
   const size_t per = (g.n + gridDim.x - 1) / gridDim.x;
   const size_t p_end = std::min(g.n, (size_t)(blockIdx.x + 1) * per);
@@ -491,7 +495,125 @@ __global__ __launch_bounds__(kBlock) void crc32_arena_lines_kernel(const uint8_t
   arena_line_pass<PROBE>(base, ar, blockIdx.x, gridDim.x, lds4, img_slice, img_group8, img_sb);
 }
 
+// Extent of a variable batch (crc32_kernels.h launch_extent): grid-stride partials per block, the last
+// block to finish reduces them, resets the arrival counter for the stream's next call and publishes.
+// ws layout (uint64): [0] arrival counter, [1..4] result {lo, hi, sum, bad}, [8 + 4b ...] block b's partial.
+constexpr int kExtentBlock = 256;
+constexpr uint32_t kExtentMaxBlocks = (kExtentScratchBytes / 8 - 8) / 4;
+__device__ __forceinline__ uint64_t wave_min(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v = min(v, (uint64_t)__shfl_xor((unsigned long long)v, d));
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_max(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v = max(v, (uint64_t)__shfl_xor((unsigned long long)v, d));
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) v += (uint64_t)__shfl_xor((unsigned long long)v, d);
+  return v;
+}
+
+__global__ __launch_bounds__(kExtentBlock) void crc32_extent_kernel(const uint64_t* __restrict__ off,
+                                                                    const uint32_t* __restrict__ len, size_t n,
+                                                                    uint64_t* ws, ExtentHint* host, uint64_t seq) {
+  __shared__ uint64_t red[4][kExtentBlock / 64];
+  __shared__ bool last;
+  uint64_t lo = ~0ull, hi = 0, sum = 0, bad = 0;
+  for (size_t i = blockIdx.x * (size_t)kExtentBlock + threadIdx.x; i < n; i += (size_t)gridDim.x * kExtentBlock) {
+    const uint64_t o = off[i], l = len[i];
+    if (l) {
+      lo = min(lo, o);
+      hi = max(hi, o + l);
+      sum += l;
+    }
+    if (i + 1 < n) {
+      const uint64_t o2 = off[i + 1];
+      bad |= (o2 < o || o2 - (o + l) >= 4096 && o2 >= o + l) ? 1u : 0u;
+    }
+  }
+  lo = wave_min(lo);
+  hi = wave_max(hi);
+  sum = wave_sum(sum);
+  bad = wave_max(bad);
+  const uint32_t w = threadIdx.x >> 6;
+  if ((threadIdx.x & 63) == 0) {
+    red[0][w] = lo;
+    red[1][w] = hi;
+    red[2][w] = sum;
+    red[3][w] = bad;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < kExtentBlock / 64; k++) {
+      lo = min(lo, red[0][k]);
+      hi = max(hi, red[1][k]);
+      sum += red[2][k];
+      bad = max(bad, red[3][k]);
+    }
+    uint64_t* part = ws + 8 + 4 * (size_t)blockIdx.x;
+    part[0] = lo;
+    part[1] = hi;
+    part[2] = sum;
+    part[3] = bad;
+    __threadfence();
+    last = atomicAdd(reinterpret_cast<unsigned long long*>(ws), 1ull) == gridDim.x - 1;
+  }
+  __syncthreads();  // also: thread 0 is done reading red
+  if (!last) return;
+  // the last block: every partial is published (each block fenced before arriving)
+  __threadfence();
+  lo = ~0ull, hi = 0, sum = 0, bad = 0;
+  for (uint32_t b = threadIdx.x; b < gridDim.x; b += kExtentBlock) {
+    const volatile uint64_t* part = ws + 8 + 4 * (size_t)b;
+    lo = min(lo, (uint64_t)part[0]);
+    hi = max(hi, (uint64_t)part[1]);
+    sum += part[2];
+    bad = max(bad, (uint64_t)part[3]);
+  }
+  lo = wave_min(lo);
+  hi = wave_max(hi);
+  sum = wave_sum(sum);
+  bad = wave_max(bad);
+  if ((threadIdx.x & 63) == 0) {
+    red[0][w] = lo;
+    red[1][w] = hi;
+    red[2][w] = sum;
+    red[3][w] = bad;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int k = 1; k < kExtentBlock / 64; k++) {
+      lo = min(lo, red[0][k]);
+      hi = max(hi, red[1][k]);
+      sum += red[2][k];
+      bad = max(bad, red[3][k]);
+    }
+    ws[1] = lo;
+    ws[2] = hi;
+    ws[3] = sum;
+    ws[4] = bad;
+    ws[0] = 0;  // the arrival counter, for this stream's next call
+    host->lo = lo;
+    host->hi = hi;
+    host->sum = sum;
+    host->bad = bad;
+    __hip_atomic_store(&host->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 }  // namespace
+
+hipError_t launch_extent(const uint64_t* off, const uint32_t* len, size_t n, void* ws, ExtentHint* host, uint64_t seq,
+                         size_t max_blocks, hipStream_t stream) {
+  size_t blocks = (n + 4 * kExtentBlock - 1) / (4 * kExtentBlock);
+  blocks = std::max<size_t>(1, std::min<size_t>({blocks, max_blocks, (size_t)kExtentMaxBlocks}));
+  hipLaunchKernelGGL(crc32_extent_kernel, dim3((unsigned)blocks), dim3(kExtentBlock), 0, stream, off, len, n,
+                     static_cast<uint64_t*>(ws), host, seq);
+  return hipGetLastError();
+}
 
 LineOut line_out(const ArenaLaunch& a, const ArenaGeom& geo) {
   LineOut ar;
@@ -509,6 +631,9 @@ LineOut line_out(const ArenaLaunch& a, const ArenaGeom& geo) {
   ar.fs0 = a.fs0;
   ar.fs1 = a.fs1;
   ar.zero_line = (uint64_t)(uintptr_t)a.zero_line;
+  ar.check = a.check;
+  ar.check_lo = a.check_lo;
+  ar.check_hi = a.check_hi;
   return ar;
 }
 
@@ -537,6 +662,9 @@ StitchGeo stitch_geo(const ArenaLaunch& a, const ArenaGeom& geo) {
   s.n = a.n;
   s.zero_line = (uint64_t)(uintptr_t)a.zero_line;
   s.out = a.out;
+  s.check = a.check;
+  s.check_lo = a.check_lo;
+  s.check_hi = a.check_hi;
   return s;
 }
 

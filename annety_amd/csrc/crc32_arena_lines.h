@@ -15,7 +15,14 @@ struct LineOut {
   uint64_t W;  // line-pass waves = 8 * workgroups
   uint64_t byte_lo, byte_hi, line_lo, line_hi, sb0, nsb, fs0, fs1;
   uint64_t zero_line;
+  const uint64_t* check;  // ArenaLaunch::check
+  uint64_t check_lo, check_hi;
 };
+
+// ArenaLaunch::check: this call's extent (ExtentResult) equals the declared one and the batch is safe.
+__device__ __forceinline__ bool extent_matches(const uint64_t* check, uint64_t lo, uint64_t hi) {
+  return !check || (check[0] == lo && check[1] == hi && check[3] == 0);
+}
 
 //   PROBE (microbench only; product = 0): bit 0 drops the S stores, bit 1 the superblock scan - wrong
 //   outputs, used to measure what those stages cost.
@@ -34,6 +41,7 @@ __device__ __forceinline__ void arena_line_pass(const uint8_t* __restrict__ base
                                                 const uint4* __restrict__ img_group8,
                                                 const uint4* __restrict__ img_sb) {
   constexpr int BLK = kBlock, VWG = kVwg;
+  if (!extent_matches(ar.check, ar.check_lo, ar.check_hi)) return;  // uniform over the grid: the stitch folds directly
   const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
   const uint32_t j = threadIdx.x & 7;
   const size_t gid = (((size_t)bid + (size_t)nbid * (threadIdx.x / VWG)) * VWG + threadIdx.x % VWG) / 8;

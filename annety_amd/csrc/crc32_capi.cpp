@@ -331,12 +331,28 @@ struct DeviceCtx {
     uint64_t tick = 0;           // last use, for LRU hand-over
     hipEvent_t fence = nullptr;  // recorded on `last` only when the slot is handed to another stream
                                  // (per-thread handles: after every call, see scratch_done)
+    // automatic variable-path choice (run_var_auto): the extent kernel's area is the slot's first
+    // kExtentScratchBytes (its arrival counter zeroed when the slot is allocated); the paths' scratch follows
+    ExtentHint* hint = nullptr;  // pinned: the extent of this slot's latest completed auto call
+    uint64_t calls = 0;          // extent kernels launched from this slot (hint->seq numbers them)
+    struct Key {
+      const void *base, *off, *len;
+      size_t n;
+      bool update;
+      bool operator==(const Key& o) const {
+        return base == o.base && off == o.off && len == o.len && n == o.n && update == o.update;
+      }
+    } key{};
+    uint64_t key_since = 0;                 // first call (seq) with the current key
+    uint64_t seen_seq = 0, prev_seq = 0;    // the two latest completed hints read for this key
+    ExtentHint seen{}, prev{};
   };
   std::mutex arena_mu;  // held while a call picks a slot and enqueues its launches
   std::vector<std::unique_ptr<ScratchSlot>> slots;
   uint64_t tick = 0;
   // test-visible counters (annety_crc_scratch_stats)
   std::atomic<uint64_t> handoffs{0}, device_syncs{0};
+  std::atomic<uint64_t> auto_arena{0}, auto_sorted{0};  // run_var_auto's choices
 };
 
 constexpr int kMaxDev = 64;
@@ -547,7 +563,8 @@ int scratch_slot(DeviceCtx& c, hipStream_t stream, size_t bytes, DeviceCtx::Scra
     if (slot->ptr) HIP_TRY(hipFreeAsync(slot->ptr, stream));
     slot->ptr = nullptr;
     slot->bytes = 0;
-    HIP_TRY(hipMallocAsync(&slot->ptr, bytes, stream));
+    HIP_TRY(hipMallocAsync(&slot->ptr, kExtentScratchBytes + bytes, stream));
+    HIP_TRY(hipMemsetAsync(slot->ptr, 0, 8, stream));  // the extent kernel's arrival counter
     slot->bytes = bytes;
   }
   slot->last = stream;
@@ -556,6 +573,9 @@ int scratch_slot(DeviceCtx& c, hipStream_t stream, size_t bytes, DeviceCtx::Scra
   *out = slot;
   return ANNETY_CRC_OK;
 }
+
+// The paths' scratch inside a slot (after the extent kernel's area).
+char* path_scratch(const DeviceCtx::ScratchSlot* slot) { return static_cast<char*>(slot->ptr) + kExtentScratchBytes; }
 
 // After the call's launches on `stream` (arena_mu still held). hipStreamPerThread resolves to the calling
 // thread's stream, which no other thread can name when it takes the slot over: such slots record their
@@ -568,15 +588,18 @@ int scratch_done(DeviceCtx::ScratchSlot* slot, hipStream_t stream) {
 
 // Variable batch: bucket by line count on the device (no host round trip), then one launch per
 // length class with its own lane-group width. Scratch: the stream's slot (scratch_slot).
-int run_var_sorted(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_off, const uint32_t* d_len,
-                   uint32_t* d_out, hipStream_t stream, bool update = false) {
+size_t sorted_scratch_bytes(size_t n) {
   const size_t rows_words = (size_t)bucket_blocks(n) * bucket_count();
-  const size_t head = (rows_words + 8) * sizeof(uint32_t);  // rows + ranges (16-byte multiple)
-  std::lock_guard<std::mutex> lk(c.arena_mu);
-  DeviceCtx::ScratchSlot* slot = nullptr;
-  int rc = scratch_slot(c, stream, head + 16 * n, &slot);
-  if (rc) return rc;
-  char* scratch = static_cast<char*>(slot->ptr);
+  return (rows_words + 8) * sizeof(uint32_t) + 16 * n;  // rows + ranges (16-byte multiple) + descriptors
+}
+
+// The sorted path's launches into `slot` (sized by sorted_scratch_bytes; c.arena_mu held).
+int run_var_sorted_in(DeviceCtx& c, DeviceCtx::ScratchSlot* slot, const void* d_base, size_t n, const uint64_t* d_off,
+                      const uint32_t* d_len, uint32_t* d_out, hipStream_t stream, bool update) {
+  const size_t rows_words = (size_t)bucket_blocks(n) * bucket_count();
+  const size_t head = (rows_words + 8) * sizeof(uint32_t);
+  int rc = ANNETY_CRC_OK;
+  char* scratch = path_scratch(slot);
   uint32_t* rows = reinterpret_cast<uint32_t*>(scratch);
   uint32_t* ranges = rows + rows_words;
   void* desc = scratch + head;
@@ -585,6 +608,16 @@ int run_var_sorted(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d
   const uint32_t groups[3] = {32, 16, 4};  // lanes per payload of the long / middle / small class
   for (int k = 0; k < 3 && rc == ANNETY_CRC_OK; k++)
     rc = run_var(c, d_base, n, 0, 0, groups[k], desc, ranges + 2 * k, d_out, stream, update);
+  return rc;
+}
+
+int run_var_sorted(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_off, const uint32_t* d_len,
+                   uint32_t* d_out, hipStream_t stream, bool update = false) {
+  std::lock_guard<std::mutex> lk(c.arena_mu);
+  DeviceCtx::ScratchSlot* slot = nullptr;
+  int rc = scratch_slot(c, stream, sorted_scratch_bytes(n), &slot);
+  if (rc) return rc;
+  rc = run_var_sorted_in(c, slot, d_base, n, d_off, d_len, d_out, stream, update);
   const int rd = scratch_done(slot, stream);
   return rc ? rc : rd;
 }
@@ -593,7 +626,7 @@ int run_var_sorted(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d
 // then one lane per payload. Scratch (S quads, S_edge, SB: ~33 words per 1 KiB block, ~3.3 % of the
 // arena) comes from the stream-ordered allocator.
 // Arena geometry and images for [d_base, d_base + arena_bytes) (everything but the batch and scratch).
-void arena_fill(const DeviceCtx& c, const void* d_base, size_t arena_bytes, ArenaLaunch& a) {
+void arena_fill_range(const DeviceCtx& c, const void* d_base, uint64_t byte_lo, uint64_t byte_hi, ArenaLaunch& a) {
   a.base = d_base;
   a.img_slice = c.d_slice;
   a.img_group8 = group_image(c, 8);
@@ -601,9 +634,9 @@ void arena_fill(const DeviceCtx& c, const void* d_base, size_t arena_bytes, Aren
   a.img_stitch = c.d_stitch;
   a.zero_line = c.d_zero;
   a.max_blocks = grid_cus(c);
-  if (!arena_bytes) return;
-  a.byte_lo = (uint64_t)(uintptr_t)d_base;
-  a.byte_hi = a.byte_lo + arena_bytes;
+  if (byte_hi <= byte_lo) return;
+  a.byte_lo = byte_lo;
+  a.byte_hi = byte_hi;
   a.line_lo = a.byte_lo >> 7;
   a.line_hi = (a.byte_hi - 1) >> 7;
   a.sb0 = a.line_lo >> 6;
@@ -611,6 +644,11 @@ void arena_fill(const DeviceCtx& c, const void* d_base, size_t arena_bytes, Aren
   a.fs0 = (a.byte_lo + 8191) >> 13;  // superblocks wholly inside the arena
   a.fs1 = a.byte_hi >> 13;
   if (a.fs1 < a.fs0) a.fs1 = a.fs0;
+}
+
+void arena_fill(const DeviceCtx& c, const void* d_base, size_t arena_bytes, ArenaLaunch& a) {
+  const uint64_t lo = (uint64_t)(uintptr_t)d_base;
+  arena_fill_range(c, d_base, lo, lo + arena_bytes, a);
 }
 
 int run_arena(DeviceCtx& c, const void* d_base, size_t arena_bytes, const uint64_t* d_off, const uint32_t* d_len,
@@ -632,11 +670,102 @@ int run_arena(DeviceCtx& c, const void* d_base, size_t arena_bytes, const uint64
   DeviceCtx::ScratchSlot* slot = nullptr;
   const int rc = scratch_slot(c, stream, bytes, &slot);
   if (rc) return rc;
-  a.scratch = static_cast<uint32_t*>(slot->ptr);
+  a.scratch = reinterpret_cast<uint32_t*>(path_scratch(slot));
   const hipError_t e = launch_arena(a, stream);
   const int rd = scratch_done(slot, stream);
   if (e != hipSuccess) return hip_fail(e);
   return rd;
+}
+
+// ---- automatic choice between the arena and the sorted path (annety_crc32_batch_var) ----
+// The arena path needs its extent on the host (grid, scratch) but the offsets are device data; reading them
+// back would make every call synchronous. Instead every call launches the extent kernel (crc32_kernels.h
+// launch_extent, ~2-3 us), which leaves the batch's extent in a pinned record per stream slot, and a call
+// takes the arena path over [lo, hi) when the two latest completed records for the same (base, offsets,
+// lengths, n) agree, are safe (sorted starts, gaps < 4 KiB) and dense (payload bytes >= 2/3 of the span).
+// The kernels then check this call's own extent against [lo, hi) on the device and, if it differs, read
+// nothing outside the payloads (each is folded directly) - a stale record costs time, never correctness
+// or a read of unmapped memory. Otherwise the sorted path runs. ANNETY_CRC_VAR_AUTO=0 keeps the sorted
+// path always.
+bool var_auto() {
+  static const bool on = [] {
+    const char* e = std::getenv("ANNETY_CRC_VAR_AUTO");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+constexpr size_t kAutoMinPayloads = 1024;  // below this the extent kernel is not worth its launch
+
+// Reads the slot's pinned record; true if a new completed one for the current key arrived.
+bool poll_hint(DeviceCtx::ScratchSlot* s) {
+  const uint64_t seq = __atomic_load_n(&s->hint->seq, __ATOMIC_ACQUIRE);
+  if (seq <= s->seen_seq || seq < s->key_since) return false;
+  ExtentHint h{};
+  h.lo = s->hint->lo;
+  h.hi = s->hint->hi;
+  h.sum = s->hint->sum;
+  h.bad = s->hint->bad;
+  if (__atomic_load_n(&s->hint->seq, __ATOMIC_ACQUIRE) != seq) return false;  // rewritten meanwhile: next call
+  h.seq = seq;
+  if (s->seen_seq >= s->key_since) {
+    s->prev = s->seen;
+    s->prev_seq = s->seen_seq;
+  }
+  s->seen = h;
+  s->seen_seq = seq;
+  return true;
+}
+
+int run_var_auto(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_off, const uint32_t* d_len,
+                 uint32_t* d_out, hipStream_t stream, bool update) {
+  if (!var_auto() || n < kAutoMinPayloads) return run_var_sorted(c, d_base, n, d_off, d_len, d_out, stream, update);
+  std::lock_guard<std::mutex> lk(c.arena_mu);
+  DeviceCtx::ScratchSlot* slot = nullptr;
+  int rc = scratch_slot(c, stream, sorted_scratch_bytes(n), &slot);
+  if (rc) return rc;
+  if (!slot->hint) {
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&slot->hint), sizeof(ExtentHint), hipHostMallocCoherent | hipHostMallocMapped));
+    std::memset(slot->hint, 0, sizeof(ExtentHint));
+  }
+  const DeviceCtx::ScratchSlot::Key key{d_base, d_off, d_len, n, update};
+  if (!(key == slot->key)) {
+    slot->key = key;
+    slot->key_since = slot->calls + 1;
+    slot->seen_seq = slot->prev_seq = 0;
+  }
+  poll_hint(slot);
+  const ExtentHint& h = slot->seen;
+  const bool arena = slot->seen_seq >= slot->key_since && slot->prev_seq >= slot->key_since && !h.bad &&
+                     h.hi > h.lo && h.lo == slot->prev.lo && h.hi == slot->prev.hi && !slot->prev.bad &&
+                     h.sum * 3 >= (h.hi - h.lo) * 2;
+  ArenaLaunch a{};
+  if (arena) {
+    const uint64_t b = (uint64_t)(uintptr_t)d_base;
+    arena_fill_range(c, d_base, b + h.lo, b + h.hi, a);
+    a.off = d_off;
+    a.len = d_len;
+    a.n = n;
+    a.out = d_out;
+    a.update = update;
+    a.check_lo = h.lo;
+    a.check_hi = h.hi;
+    if (a.nsb && (rc = scratch_slot(c, stream, arena_geom(a).words * sizeof(uint32_t), &slot))) return rc;
+  }
+  // this call's extent: the next calls' record, and the check the arena launches make
+  const uint64_t seq = ++slot->calls;
+  hipError_t e = launch_extent(d_off, d_len, n, slot->ptr, slot->hint, seq, grid_cus(c), stream);
+  if (e != hipSuccess) return hip_fail(e);
+  (arena ? c.auto_arena : c.auto_sorted)++;
+  if (arena) {
+    a.check = extent_result(slot->ptr);
+    a.scratch = reinterpret_cast<uint32_t*>(path_scratch(slot));
+    e = launch_arena(a, stream);
+    rc = e == hipSuccess ? ANNETY_CRC_OK : hip_fail(e);
+  } else {
+    rc = run_var_sorted_in(c, slot, d_base, n, d_off, d_len, d_out, stream, update);
+  }
+  const int rd = scratch_done(slot, stream);
+  return rc ? rc : rd;
 }
 
 bool fixed_fast_ok(const void* d_base, size_t len, size_t stride) {
@@ -718,7 +847,7 @@ int run_split(DeviceCtx& c, const void* d_base, size_t n, uint64_t len, uint64_t
   std::lock_guard<std::mutex> lk(c.arena_mu);
   DeviceCtx::ScratchSlot* slot = nullptr;
   if ((rc = scratch_slot(c, stream, 16 + crc_bytes + 16 * tasks, &slot))) return rc;
-  char* scratch = static_cast<char*>(slot->ptr);
+  char* scratch = path_scratch(slot);
   uint32_t* range = reinterpret_cast<uint32_t*>(scratch);
   uint32_t* seg_crc = reinterpret_cast<uint32_t*>(scratch + 16);
   void* desc = scratch + 16 + crc_bytes;
@@ -800,6 +929,7 @@ int annety_crc_shutdown(void) {
       }
       for (auto& sl : c.slots) {
         if (sl->ptr) (void)hipFree(sl->ptr);
+        if (sl->hint) (void)hipHostFree(sl->hint);
         (void)hipEventDestroy(sl->fence);
       }
       c.slots.clear();
@@ -851,6 +981,13 @@ int annety_crc_scratch_stats(int device, uint64_t* slots, uint64_t* handoffs, ui
   return ANNETY_CRC_OK;
 }
 
+int annety_crc_var_path_stats(int device, uint64_t* arena, uint64_t* sorted) {
+  if (device < 0 || device >= kMaxDev) return ANNETY_CRC_ENODEV;
+  if (arena) *arena = g_dev[device].auto_arena.load();
+  if (sorted) *sorted = g_dev[device].auto_sorted.load();
+  return ANNETY_CRC_OK;
+}
+
 int annety_crc_stream_release(void* stream) {
   hipStream_t s = static_cast<hipStream_t>(stream);
   DeviceCtx* c = nullptr;
@@ -862,6 +999,10 @@ int annety_crc_stream_release(void* stream) {
     if (!same_owner(sl, s)) continue;
     // stream-ordered: the memory returns to the pool after the stream's queued work, nobody waits
     if (sl.ptr) HIP_TRY(hipFreeAsync(sl.ptr, s));
+    if (sl.hint) {  // the stream's queued extent kernels may still write it: wait for them first
+      HIP_TRY(hipStreamSynchronize(s));
+      (void)hipHostFree(sl.hint);
+    }
     (void)hipEventDestroy(sl.fence);
     c->slots.erase(c->slots.begin() + (long)i);
     break;
@@ -931,7 +1072,7 @@ int annety_crc32_batch_var(const void* d_base, const uint64_t* d_off, const uint
   int rc = stream_ctx(static_cast<hipStream_t>(stream), &c);
   if (rc) return rc;
   if (n > 0xFFFFFFFFull) return ANNETY_CRC_EINVAL;  // order[] holds 32-bit payload indices
-  return run_var_sorted(*c, d_base, n, d_off, d_len, d_out, static_cast<hipStream_t>(stream));
+  return run_var_auto(*c, d_base, n, d_off, d_len, d_out, static_cast<hipStream_t>(stream), false);
 }
 
 int annety_crc32_batch_var_arena(const void* d_arena, size_t arena_bytes, const uint64_t* d_off,
@@ -978,7 +1119,7 @@ int annety_crc32_update_batch_var(uint32_t* d_state, const void* d_base, const u
   DeviceCtx* c = nullptr;
   int rc = stream_ctx(static_cast<hipStream_t>(stream), &c);
   if (rc) return rc;
-  return run_var_sorted(*c, d_base, n, d_off, d_len, d_state, static_cast<hipStream_t>(stream), true);
+  return run_var_auto(*c, d_base, n, d_off, d_len, d_state, static_cast<hipStream_t>(stream), true);
 }
 
 // Staging ring of the current device's context, allocated for at least `need` bytes per slot.

@@ -86,7 +86,28 @@ struct ArenaLaunch {
   uint32_t* out;             // digests, or (update) registers in place
   size_t max_blocks;
   bool update;
+  // automatic path selection (annety_crc32_batch_var): the arena was declared from an earlier call's
+  // extent; both launches check this call's extent (ExtentResult, written by launch_extent on the same
+  // stream) against [check_lo, check_hi) first - on any difference the line pass does nothing and every
+  // payload is folded directly from its own bytes (no read outside the payloads). null = no check.
+  const uint64_t* check;
+  uint64_t check_lo, check_hi;
 };
+
+// Extent of a variable batch, for the automatic choice between the arena and the sorted path: over the
+// non-empty payloads lo = min offset, hi = max end, sum = total bytes; bad != 0 unless every payload starts
+// at or after the previous one and within 4 KiB of its end (then every byte of [lo, hi) lies on a page that
+// also holds payload bytes, so the arena path reads only mapped memory). ExtentResult = {lo, hi, sum, bad}.
+// Written to the device scratch `ws` (kExtentScratchBytes, its counter zeroed once when allocated) and,
+// with `seq` last (release, system scope), to the pinned host record `host` (ExtentHint).
+constexpr size_t kExtentScratchBytes = 16384;
+struct ExtentHint {
+  uint64_t lo, hi, sum, bad;
+  uint64_t seq;
+};
+hipError_t launch_extent(const uint64_t* off, const uint32_t* len, size_t n, void* ws, ExtentHint* host,
+                         uint64_t seq, size_t max_blocks, hipStream_t stream);
+inline const uint64_t* extent_result(const void* ws) { return static_cast<const uint64_t*>(ws) + 1; }
 
 // Line-pass layout. L line-pass workgroups of 512 lanes = W = 8L waves = 64L lane groups;
 // wave w's task t is full superblock fs0 + t*W + w (lane group g = 8w + block). Per line of a full

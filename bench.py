@@ -60,9 +60,10 @@ def parse():
     p.add_argument("--strong", action="store_true",
                    help="fixed configs: --payloads (default 1M) is the TOTAL over all ranks, split into contiguous "
                         "shards (strong scaling); default is per GPU (weak scaling)")
-    p.add_argument("--var-path", choices=["arena", "sorted"], default="arena",
+    p.add_argument("--var-path", choices=["arena", "auto", "sorted"], default="arena",
                    help="config 3: arena = one pass over the packed arena + per-payload stitch (annety_crc32_batch_var_arena); "
-                        "sorted = the general length-bucketed path (annety_crc32_batch_var)")
+                        "auto = annety_crc32_batch_var, which picks the arena path itself from the batch's recorded extent; "
+                        "sorted = the length-bucketed path only (ANNETY_CRC_VAR_AUTO=0)")
     p.add_argument("--chunks", type=int, default=None,
                    help="N>1: chunks per shard for the pipelined gather (default 1 for config 1: step s's gather "
                         "overlaps step s+1's kernel; 2 for config 4, one-rank rehearsal 1/2/4 chunks "
@@ -217,12 +218,16 @@ class Workload:
             self.payload_bytes = total
             self.algo_bytes = total + 4 * self.n + 12 * self.n  # + offset/length metadata reads
             self.arena = args.var_path == "arena"
+            self.var_path = args.var_path
             self.kernel = ("crc32_arena_lines_kernel + crc32_arena_stitch_kernel, one step "
                            "(annety_amd/csrc/crc32_arena.hip, crc32_arena_lines.h)" if self.arena else
+                           "crc32_extent_kernel + (arena or sorted path, chosen per call), one step "
+                           "(annety_amd/csrc/crc32_capi.cpp run_var_auto)" if args.var_path == "auto" else
                            "crc32_bucket_hist/scan/scatter + crc32_var_kernel<32/8/2>, one step "
                            "(annety_amd/csrc/crc32_kernels.hip)")
             self.desc = (f"BASELINE config 3: {self.n} payloads, Zipf(1.1) lengths 64 B-64 KiB packed unaligned, "
-                         f"{total / 2**30:.3f} GiB per GPU, " + ("arena path" if self.arena else "sorted path"))
+                         f"{total / 2**30:.3f} GiB per GPU, " + {"arena": "arena path", "auto": "automatic path choice",
+                                                                  "sorted": "sorted path"}[args.var_path])
         # strong scaling: shards differ by at most one payload; the digest buffer is padded (zeros) to the
         # largest so that every rank's gather moves the same count
         self.n_pad = -(-self.n_total // world) if getattr(args, "strong", False) else self.n
@@ -450,6 +455,8 @@ def main():
         raise SystemExit("--strong applies to the fixed 1 KiB configs (1, 4)")
     if args.chunks is None:
         args.chunks = 2 if args.config == 4 else 1
+    if args.var_path == "sorted":
+        os.environ["ANNETY_CRC_VAR_AUTO"] = "0"  # read once by the library: before it loads
     if multi and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < args.hw_queues:
         # HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default); the compute stream, torch's
         # RCCL stream and RCCL's own streams then share queues, and a queue runs its packets in order. Set

@@ -71,6 +71,9 @@ int annety_crc_stream_release(void* stream);
 /* Scratch bookkeeping of `device` (test and tuning visibility): streams holding a slot, hand-overs of a
  * slot between streams so far, device-wide synchronisations so far (0 outside annety_crc_shutdown). */
 int annety_crc_scratch_stats(int device, uint64_t* slots, uint64_t* handoffs, uint64_t* device_syncs);
+/* Calls of annety_crc32_batch_var / annety_crc32_update_batch_var on `device` (n >= 1024) that took the
+ * arena path and the sorted path so far (the automatic choice; test and tuning visibility). */
+int annety_crc_var_path_stats(int device, uint64_t* arena, uint64_t* sorted);
 
 /* ---- host scalar API: exact replacements of the reference's inline methods ----
  * annety_crc32_long   replaces Crc32c::crc32_long(const char*, size_t)   include/Crc32c.h:58-69
@@ -94,7 +97,13 @@ const uint32_t* annety_crc32_table256(void);
  * Asynchronous with respect to the host: results are valid after the stream is synchronised. */
 int annety_crc32_batch_fixed(const void* d_base, size_t n, size_t len, size_t stride, uint32_t* d_out,
                              void* stream);
-/* Variable length: payload i = [d_base + d_off[i], + d_len[i]) (any alignment). */
+/* Variable length: payload i = [d_base + d_off[i], + d_len[i]) (any alignment).
+ * Path choice is automatic: every call also records the batch's extent on the device (a few us), and once
+ * two completed calls on the same stream with the same (d_base, d_off, d_len, n) have shown a dense, sorted
+ * batch (starts ascending, gaps < 4 KiB, payload bytes >= 2/3 of the span) the call runs the arena path over
+ * that span; otherwise (and for n < 1024) the length-sorted path. The arena launches re-check the call's
+ * own extent on the device, so a batch whose layout changed under the same pointers is still exact (its
+ * payloads are then folded directly, more slowly, for that call). ANNETY_CRC_VAR_AUTO=0: sorted path only. */
 int annety_crc32_batch_var(const void* d_base, const uint64_t* d_off, const uint32_t* d_len, size_t n,
                            uint32_t* d_out, void* stream);
 /* Raw-register update (crc32_update semantics) for a fixed-length batch: d_state[i] is the register

@@ -1,0 +1,117 @@
+"""Automatic path choice of annety_crc32_batch_var / annety_crc32_update_batch_var (crc32_capi.cpp
+run_var_auto): every call records its batch's extent on the device; once two completed calls on a stream
+with the same pointers showed a dense sorted batch the arena path runs, re-checking each call's own extent on
+the device. Digests are checked against the oracle on every call, also when the layout changes under the
+same pointers (the arena launches then fold each payload directly) and for sparse batches (sorted path)."""
+import numpy as np
+import pytest
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+
+def _packed(seed, n, gap=0):
+    rng = np.random.default_rng(seed)
+    lens = np.minimum(65536, 64 * rng.zipf(1.3, n) + rng.integers(0, 64, n)).astype(np.int64)
+    offs = np.concatenate([[0], np.cumsum(lens + gap)[:-1]]).astype(np.int64)
+    data = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 256, dtype=np.uint8)
+    return data, offs, lens
+
+
+def _dev(gpu, data, offs, lens):
+    import torch
+
+    return (torch.from_numpy(data).to(gpu), torch.from_numpy(offs).to(gpu),
+            torch.from_numpy(lens.astype(np.int32)).to(gpu))
+
+
+def _check(out, data, offs, lens):
+    import torch
+
+    torch.cuda.synchronize()
+    want = oracle.batch_var(data, offs.astype(np.uint64), lens.astype(np.uint32))
+    got = out.cpu().numpy().view(np.uint32)
+    assert np.array_equal(got, want), int((got != want).sum())
+
+
+def test_dense_batch_moves_to_arena(gpu):
+    import torch
+
+    import annety_amd
+
+    data, offs, lens = _packed(1, 5000)
+    d, o, ln = _dev(gpu, data, offs, lens)
+    out = torch.empty(len(lens), dtype=torch.int32, device=gpu)
+    s0 = annety_amd.var_path_stats(0)
+    for i in range(6):
+        out.zero_()
+        annety_amd.crc32_batch_var(d, o, ln, out=out)
+        _check(out, data, offs, lens)  # synchronises: this call's extent record is complete
+    s1 = annety_amd.var_path_stats(0)
+    assert s1["sorted"] - s0["sorted"] == 2 and s1["arena"] - s0["arena"] == 4, (s0, s1)
+    # back to back without waiting: every digest still exact
+    outs = [torch.empty(len(lens), dtype=torch.int32, device=gpu) for _ in range(8)]
+    for x in outs:
+        annety_amd.crc32_batch_var(d, o, ln, out=x)
+    for x in outs:
+        _check(x, data, offs, lens)
+
+
+def test_sparse_batch_stays_sorted(gpu):
+    import torch
+
+    import annety_amd
+
+    data, offs, lens = _packed(2, 3000, gap=5000)  # gaps >= 4 KiB: never the arena path
+    d, o, ln = _dev(gpu, data, offs, lens)
+    out = torch.empty(len(lens), dtype=torch.int32, device=gpu)
+    s0 = annety_amd.var_path_stats(0)
+    for _ in range(4):
+        annety_amd.crc32_batch_var(d, o, ln, out=out)
+        _check(out, data, offs, lens)
+    s1 = annety_amd.var_path_stats(0)
+    assert s1["arena"] == s0["arena"] and s1["sorted"] - s0["sorted"] == 4
+
+
+def test_layout_changes_under_the_same_pointers(gpu):
+    """The arena path is chosen from earlier calls; then the offsets are rewritten in place (a shifted dense
+    layout, then one with a 6 KiB gap, then unsorted): the device check sees the difference and every digest
+    stays exact."""
+    import torch
+
+    import annety_amd
+
+    data, offs, lens = _packed(3, 4000)
+    data = np.concatenate([data, np.zeros(70000, dtype=np.uint8)])  # room for every variant below
+    d, o, ln = _dev(gpu, data, offs, lens)
+    out = torch.empty(len(lens), dtype=torch.int32, device=gpu)
+    for _ in range(4):
+        annety_amd.crc32_batch_var(d, o, ln, out=out)
+        _check(out, data, offs, lens)
+    a0 = annety_amd.var_path_stats(0)["arena"]
+    variants = [offs + 200, offs.copy(), offs[::-1].copy()]
+    variants[1][len(offs) // 2:] += 6000  # one 6 KiB gap
+    for v in variants:
+        o.copy_(torch.from_numpy(v))  # same pointers, new layout
+        annety_amd.crc32_batch_var(d, o, ln, out=out)
+        _check(out, data, v, lens)
+    assert annety_amd.var_path_stats(0)["arena"] > a0  # the first changed call still took the (checked) arena path
+
+
+def test_update_mode_auto(gpu):
+    """Streaming registers through the automatic path: the same fragment layout every call (a receive ring),
+    registers carried across calls, equal to the oracle's crc32_update chain."""
+    import torch
+
+    import annety_amd
+
+    data, offs, lens = _packed(4, 2000)
+    d, o, ln = _dev(gpu, data, offs, lens)
+    state = torch.full((len(lens),), -1, dtype=torch.int32, device=gpu)
+    want = np.full(len(lens), 0xFFFFFFFF, dtype=np.uint32)
+    for _ in range(5):
+        annety_amd.crc32_update_batch_var(state, d, o, ln)
+        want = oracle.batch_var_mt(data, offs.astype(np.uint64), lens.astype(np.uint32), threads=8, states=want)
+        torch.cuda.synchronize()
+        assert np.array_equal(state.cpu().numpy().view(np.uint32), want)
