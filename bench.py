@@ -536,12 +536,22 @@ def main():
     if gather_ok is False:
         raise SystemExit(f"rank {rank}: gathered digests differ from the ranks' own")
 
-    def timed(steps: int, gather: bool) -> float:
+    def timed(steps: int, gather: bool):
+        """K steps bracketed by a barrier + synchronise on both sides; max over ranks. HIP events on the
+        launch stream inside the same bracket give the kernel-stream time: the roofline's launch duration and,
+        in up to 20 consecutive groups, a per-step median / min / max (with the gather on, one group: the
+        gathers' stream waits would cut across group boundaries)."""
+        ngroups = max(1, min(20, steps)) if (pipe is None or not gather) else 1
+        gsteps = [steps * (i + 1) // ngroups - steps * i // ngroups for i in range(ngroups)]
+        evs = [torch.cuda.Event(enable_timing=True) for _ in range(ngroups + 1)]
         if multi:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        run_steps(steps, gather)
+        evs[0].record(stream)
+        for i, gs in enumerate(gsteps):
+            run_steps(gs, gather)
+            evs[i + 1].record(stream)
         torch.cuda.synchronize()
         if multi:
             dist.barrier()
@@ -550,7 +560,9 @@ def main():
             t = torch.tensor([el], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
-        return el
+        kern = evs[0].elapsed_time(evs[-1]) / steps
+        per = sorted(evs[i].elapsed_time(evs[i + 1]) / gs for i, gs in enumerate(gsteps))
+        return el, kern, per
 
     t_pw = time.perf_counter()
     while time.perf_counter() - t_pw < args.prewarm_s:
@@ -560,23 +572,12 @@ def main():
     run_steps(args.warmup, True)
     torch.cuda.synchronize()
 
-    # kernel-only time on the launch stream: HIP events around the same number of steps (no gather), in
-    # up to 20 consecutive groups, so the line carries a per-step median / min / max beside the mean
-    ngroups = max(1, min(20, args.steps))
-    gsteps = [args.steps * (i + 1) // ngroups - args.steps * i // ngroups for i in range(ngroups)]
-    evs = [torch.cuda.Event(enable_timing=True) for _ in range(ngroups + 1)]
-    evs[0].record(stream)
-    for i, gs in enumerate(gsteps):
-        for _ in range(gs):
-            step(gather=False)
-        evs[i + 1].record(stream)
-    torch.cuda.synchronize()
-    kern_ms = evs[0].elapsed_time(evs[-1]) / args.steps
-    per_step = sorted(evs[i].elapsed_time(evs[i + 1]) / gs for i, gs in enumerate(gsteps))
+    elapsed, kern_ms, per_step = timed(args.steps, gather=True)
+    compute_only = None
+    if multi:  # the same steps without the gather: value_compute_only, and the roofline's kernel time
+        compute_only, kern_ms, per_step = timed(args.steps, gather=False)
     kern_median = float(np.median(per_step))
-
-    elapsed = timed(args.steps, gather=True)
-    compute_only = timed(args.steps, gather=False) if multi else None
+    ngroups = len(per_step)
 
     if rank == 0:
         # every rank's payload bytes (weak: n per GPU x world; strong: the fixed total)
