@@ -140,6 +140,11 @@ struct StitchGeo {
   uint64_t W;   // line-pass waves = 8 * L
   uint32_t L;   // line-pass workgroups (64 L lane groups)
   const uint32_t *S, *SB, *S_edge, *SB_edge;
+  // the stitch addresses the line pass's outputs as 32-bit word indices from W0 (= S; when the call has no
+  // arena, g.len: index 0 is then a valid word for the dummy loads); sb_word / edge_word = SB / S_edge - S
+  const uint32_t* W0;
+  uint32_t sb_word, edge_word;
+  uint64_t Lmagic;  // ceil(2^40 / L): (x * Lmagic) >> 40 == x / L for x < 2^26 (s_addr's task division)
   const uint64_t* off;
   const uint32_t* len;
   size_t n;
@@ -157,11 +162,11 @@ struct Plan {
   bool fast, headX, tailX;
   uint32_t lead, te;
   uint32_t hlo, hhi, tlo, thi;  // window byte ranges kept, relative to the window start
-  uint32_t m1[4], m2[4];        // step maps (seg_map index)
+  uint32_t m1, m2;              // step q's maps (seg_map index < 32) in byte q
   uint32_t act, yzero;          // per step bit: active / second operand is zero
   uint32_t nmid;
-  uint64_t mid_s;               // first whole superblock between (relative to sb0)
-  uint64_t xa[4], ya[4];        // step operand addresses
+  uint32_t mid_s;               // first whole superblock between (relative to sb0)
+  uint32_t xa[4], ya[4];        // step operand word indices from g.W0
 };
 struct Vals {
   uint4 h[4], t[4];
@@ -180,24 +185,26 @@ struct Stitcher {
   const uint32_t* lds;
   LaneCtx k;
 
-  __device__ __forceinline__ uint32_t word(uint64_t addr) const { return gload4(addr); }
-  // address of S for line a (0..7) of block rb (relative to superblock sb0)
-  __device__ __forceinline__ uint64_t s_addr(uint64_t rb, uint32_t a) const {
+  __device__ __forceinline__ uint32_t word(uint32_t idx) const {
+    return gload4((uint64_t)(uintptr_t)g.W0 + 4ull * idx);
+  }
+  // word index of S for line a (0..7) of block rb (relative to superblock sb0)
+  __device__ __forceinline__ uint32_t s_addr(uint64_t rb, uint32_t a) const {
     const uint64_t sb = g.sb0 + (rb >> 3);
     const bool edge = sb < g.fs0 || sb >= g.fs1;
-    const uint32_t r = (uint32_t)(rb - (g.fs0 - g.sb0) * 8);  // block of the full range (< 2^32: host check)
-    const uint32_t t = (r >> 6) / g.L;                        // task; lane group = r - t * 64 L
-    const uint64_t full = arena_s_word(t, r - t * 64 * g.L, a, g.W) * 4;
-    const uint64_t ed = ((sb == g.sb0 ? 0 : 64) + (rb & 7) * 8 + a) * 4;
-    return edge ? (uint64_t)(uintptr_t)g.S_edge + ed : (uint64_t)(uintptr_t)g.S + full;
+    const uint32_t r = (uint32_t)(rb - (g.fs0 - g.sb0) * 8);               // block of the full range (< 2^32)
+    const uint32_t t = (uint32_t)(((uint64_t)(r >> 6) * g.Lmagic) >> 40);  // task = (r >> 6) / L
+    const uint32_t full = (uint32_t)arena_s_word(t, r - t * 64 * g.L, a, g.W);  // lane group = r - t * 64 L
+    const uint32_t ed = g.edge_word + (sb == g.sb0 ? 0u : 64u) + (uint32_t)(rb & 7) * 8 + a;
+    return edge ? ed : full;
   }
-  // address of SB for block gg of superblock sbr (relative to sb0)
-  __device__ __forceinline__ uint64_t sb_addr(uint64_t sbr, uint32_t gg) const {
+  // word index of SB for block gg of superblock sbr (relative to sb0)
+  __device__ __forceinline__ uint32_t sb_addr(uint64_t sbr, uint32_t gg) const {
     const uint64_t sb = g.sb0 + sbr;
     const bool edge = sb < g.fs0 || sb >= g.fs1;
-    const uint64_t full = ((sb - g.fs0) * 8 + gg) * 4;
-    const uint64_t ed = ((sb == g.sb0 ? 0 : 8) + gg) * 4;
-    return edge ? (uint64_t)(uintptr_t)g.SB_edge + ed : (uint64_t)(uintptr_t)g.SB + full;
+    const uint32_t full = g.sb_word + (uint32_t)(sb - g.fs0) * 8 + gg;
+    const uint32_t ed = g.edge_word + 128u + (sb == g.sb0 ? 0u : 8u) + gg;
+    return edge ? ed : full;
   }
 
   // Phase A: descriptor, plan, window and register loads (nothing the line pass writes).
@@ -244,38 +251,38 @@ struct Stitcher {
     const uint32_t g0 = (uint32_t)B0 & 7, g1 = (uint32_t)B1 & 7;
     const bool one = s0 == s1;
     // step 0: head block (or the whole run when it stays in one block)
-    y.m1[0] = kMapF + (same ? z - a + 1 : 8 - a) - 1;
-    y.m2[0] = kMapUL + (same ? 7 - z : 0);
+    y.m1 = kMapF + (same ? z - a + 1 : 8 - a) - 1;
+    y.m2 = kMapUL + (same ? 7 - z : 0);
     y.xa[0] = s_addr(rb0, a);
     y.ya[0] = s_addr(rb0, z + 1 < 8 ? z + 1 : 0);
     const bool yz0 = !same || z == 7;
     // step 1: blocks of the first partial superblock (or all of them when they stay in one)
-    y.m1[1] = kMapG + (one ? g1 - g0 + 1 : 8 - g0) - 1;
-    y.m2[1] = kMapUB + (one ? 7 - g1 : 0);
+    y.m1 |= (kMapG + (one ? g1 - g0 + 1 : 8 - g0) - 1) << 8;
+    y.m2 |= (kMapUB + (one ? 7 - g1 : 0)) << 8;
     y.xa[1] = sb_addr(s0, g0);
     y.ya[1] = sb_addr(s0, g1 + 1 < 8 ? g1 + 1 : 0);
     const bool yz1 = !one || g1 == 7;
     // step 2: blocks 0..g1 of the last partial superblock
-    y.m1[2] = kMapG + g1;
-    y.m2[2] = kMapUB + (7 - g1);
+    y.m1 |= (kMapG + g1) << 16;
+    y.m2 |= (kMapUB + (7 - g1)) << 16;
     y.xa[2] = sb_addr(s1, 0);
     y.ya[2] = sb_addr(s1, g1 + 1 < 8 ? g1 + 1 : 0);
     const bool yz2 = g1 == 7;
     // step 3: lines 0..z of the tail block
-    y.m1[3] = kMapF + z;
-    y.m2[3] = kMapUL + (7 - z);
+    y.m1 |= (kMapF + z) << 24;
+    y.m2 |= (kMapUL + (7 - z)) << 24;
     y.xa[3] = s_addr(rb1, 0);
     y.ya[3] = s_addr(rb1, z + 1 < 8 ? z + 1 : 0);
     const bool yz3 = z == 7;
     y.act = (seg ? 1u : 0u) | (blocks ? 2u : 0u) | (blocks && !one ? 4u : 0u) | (seg && !same ? 8u : 0u);
     y.yzero = (yz0 ? 1u : 0u) | (yz1 ? 2u : 0u) | (yz2 ? 4u : 0u) | (yz3 ? 8u : 0u);
     y.nmid = blocks && !one ? (uint32_t)(s1 - s0 - 1) : 0u;
-    y.mid_s = s0 + 1;
+    y.mid_s = (uint32_t)(s0 + 1);
   }
 
   // Phase B: the S/SB words of the plan.
   __device__ __forceinline__ void plan_b(size_t p, const Plan& y, Vals& v) const {
-    const uint64_t dummy = (uint64_t)(uintptr_t)(g.len + p);
+    const uint32_t dummy = 0;  // g.W0[0]: a valid word (the loads of inactive steps are not used)
 #pragma unroll
     for (int q = 0; q < 4; q++) {
       const bool on = (y.act >> q) & 1u;
@@ -323,7 +330,8 @@ struct Stitcher {
         for (int q = 0; q < 2; q++) {
           if ((y.act >> q) & 1u) {
             const uint32_t d = v.x[q] ^ (((y.yzero >> q) & 1u) ? 0u : v.y[q]);
-            acc = seg_map<ADJ>(acc, y.m1[q], lds) ^ seg_map<ADJ>(d, y.m2[q], lds);
+            acc = seg_map<ADJ>(acc, __builtin_amdgcn_ubfe(y.m1, 8 * q, 5), lds) ^
+                  seg_map<ADJ>(d, __builtin_amdgcn_ubfe(y.m2, 8 * q, 5), lds);
           }
         }
         // whole superblocks between the partial ones: acc = shift_8KiB(acc) ^ SB[s,0]
@@ -340,7 +348,8 @@ struct Stitcher {
         for (int q = 2; q < 4; q++) {
           if ((y.act >> q) & 1u) {
             const uint32_t d = v.x[q] ^ (((y.yzero >> q) & 1u) ? 0u : v.y[q]);
-            acc = seg_map<ADJ>(acc, y.m1[q], lds) ^ seg_map<ADJ>(d, y.m2[q], lds);
+            acc = seg_map<ADJ>(acc, __builtin_amdgcn_ubfe(y.m1, 8 * q, 5), lds) ^
+                  seg_map<ADJ>(d, __builtin_amdgcn_ubfe(y.m2, 8 * q, 5), lds);
           }
         }
       }
@@ -637,8 +646,8 @@ LineOut line_out(const ArenaLaunch& a, const ArenaGeom& geo) {
   return ar;
 }
 
-size_t stitch_blocks(const ArenaLaunch& a) {
-  return std::max<size_t>(1, std::min<size_t>(a.max_blocks, (a.n + kStitchBlock - 1) / kStitchBlock));
+size_t stitch_blocks(const ArenaLaunch& a, size_t blk = kStitchBlock) {
+  return std::max<size_t>(1, std::min<size_t>(a.max_blocks, (a.n + blk - 1) / blk));
 }
 
 StitchGeo stitch_geo(const ArenaLaunch& a, const ArenaGeom& geo) {
@@ -657,6 +666,10 @@ StitchGeo stitch_geo(const ArenaLaunch& a, const ArenaGeom& geo) {
   s.SB = a.scratch ? a.scratch + geo.sb_off : nullptr;
   s.S_edge = a.scratch ? a.scratch + geo.edge_off : nullptr;
   s.SB_edge = a.scratch ? a.scratch + geo.edge_off + 128 : nullptr;
+  s.W0 = a.scratch ? a.scratch : a.len;
+  s.sb_word = (uint32_t)geo.sb_off;
+  s.edge_word = (uint32_t)geo.edge_off;
+  s.Lmagic = ((1ull << 40) + geo.blocks - 1) / geo.blocks;
   s.off = a.off;
   s.len = a.len;
   s.n = a.n;
@@ -668,18 +681,18 @@ StitchGeo stitch_geo(const ArenaLaunch& a, const ArenaGeom& geo) {
   return s;
 }
 
-template <int PROBE, int PIPE = 0>
+template <int PROBE, int PIPE = 0, int BLK = kStitchBlock>
 hipError_t launch_stitch_p(const ArenaLaunch& a, hipStream_t stream) {
   const StitchGeo s = stitch_geo(a, arena_geom(a));
-  const size_t blocks = stitch_blocks(a);
+  const size_t blocks = stitch_blocks(a, BLK);
   const uint4* img_slice = static_cast<const uint4*>(a.img_slice);
   const uint4* img_stitch = static_cast<const uint4*>(a.img_stitch);
   if (a.update)
-    hipLaunchKernelGGL((crc32_arena_stitch_kernel<true, kStitchBlock, PROBE, PIPE>), dim3((unsigned)blocks),
-                       dim3(kStitchBlock), 0, stream, s, img_slice, img_stitch);
+    hipLaunchKernelGGL((crc32_arena_stitch_kernel<true, BLK, PROBE, PIPE>), dim3((unsigned)blocks), dim3(BLK), 0,
+                       stream, s, img_slice, img_stitch);
   else
-    hipLaunchKernelGGL((crc32_arena_stitch_kernel<false, kStitchBlock, PROBE, PIPE>), dim3((unsigned)blocks),
-                       dim3(kStitchBlock), 0, stream, s, img_slice, img_stitch);
+    hipLaunchKernelGGL((crc32_arena_stitch_kernel<false, BLK, PROBE, PIPE>), dim3((unsigned)blocks), dim3(BLK), 0,
+                       stream, s, img_slice, img_stitch);
   return hipGetLastError();
 }
 
@@ -716,11 +729,16 @@ hipError_t launch_arena(const ArenaLaunch& a, hipStream_t stream) {
   // The stitch issues a lane's next payload loads before folding the current one (PIPE 1): config-3 step
   // 0.2139-0.2142 ms vs 0.2144-0.2151 without, same box, three alternating pairs
   // (profiles/r02/stitch_pipe_bench_ab/). ANNETY_CRC_STITCH_PIPE=0 selects the one-payload-at-a-time loop.
-  static const bool pipe = [] {
+  // ANNETY_CRC_STITCH_BLK=768 (A/B): 768-lane blocks, one payload in flight per lane (PIPE 0) under the
+  // 168-VGPR cap of 3 waves per SIMD, instead of 512 lanes with two payloads in flight per lane.
+  static const int mode = [] {
     const char* e = std::getenv("ANNETY_CRC_STITCH_PIPE");
-    return !(e && e[0] == '0');
+    const char* b = std::getenv("ANNETY_CRC_STITCH_BLK");
+    if (b && std::atoi(b) == 768) return 2;
+    return (e && e[0] == '0') ? 0 : 1;
   }();
-  return pipe ? launch_stitch_p<0, 1>(a, stream) : launch_stitch_p<0>(a, stream);
+  if (mode == 2) return launch_stitch_p<0, 0, 768>(a, stream);
+  return mode == 1 ? launch_stitch_p<0, 1>(a, stream) : launch_stitch_p<0>(a, stream);
 }
 
 }  // namespace annety_crc

@@ -666,6 +666,7 @@ int run_arena(DeviceCtx& c, const void* d_base, size_t arena_bytes, const uint64
     return e == hipSuccess ? ANNETY_CRC_OK : hip_fail(e);
   }
   const size_t bytes = arena_geom(a).words * sizeof(uint32_t);
+  if (bytes / sizeof(uint32_t) >= (1ull << 32)) return ANNETY_CRC_EINVAL;  // the stitch's 32-bit word indices
   std::lock_guard<std::mutex> lk(c.arena_mu);
   DeviceCtx::ScratchSlot* slot = nullptr;
   const int rc = scratch_slot(c, stream, bytes, &slot);
@@ -737,7 +738,7 @@ int run_var_auto(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_o
   const ExtentHint& h = slot->seen;
   const bool arena = slot->seen_seq >= slot->key_since && slot->prev_seq >= slot->key_since && !h.bad &&
                      h.hi > h.lo && h.lo == slot->prev.lo && h.hi == slot->prev.hi && !slot->prev.bad &&
-                     h.sum * 3 >= (h.hi - h.lo) * 2;
+                     h.sum * 3 >= (h.hi - h.lo) * 2 && h.hi - h.lo < (32ull << 30);
   ArenaLaunch a{};
   if (arena) {
     const uint64_t b = (uint64_t)(uintptr_t)d_base;

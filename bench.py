@@ -41,8 +41,8 @@ sys.path.insert(0, ROOT)
 METRIC = "CRC-32C GiB/s device-resident (1M×1KiB) @1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md (8.0 TB/s)
 # Per-launch HBM bytes measured by profiles/pmc.sh at this code (FETCH_SIZE x2 + WRITE_SIZE), per config.
-PMC_FILES = {1: "profiles/r02/config1_pmc.json", 3: "profiles/r02/config3_pmc.json",
-             2: "profiles/r02/config2_pmc.json", 4: "profiles/r02/config1_pmc.json"}
+PMC_FILES = {1: "profiles/r03/config1_pmc.json", 3: "profiles/r03/config3_pmc.json",
+             2: "profiles/r03/config2_pmc.json", 4: "profiles/r03/config1_pmc.json"}
 # The reference build of oracle/_ref (oracle/Makefile): the reference's Release flags without -march=native.
 REF_FLAGS = "g++ -std=c++11 -O2 -DNDEBUG (CMakeLists.txt:24,48 Release flags; -march=native dropped so the .so runs on any host)"
 
@@ -536,12 +536,12 @@ def main():
     if gather_ok is False:
         raise SystemExit(f"rank {rank}: gathered digests differ from the ranks' own")
 
-    def timed(steps: int, gather: bool):
+    def timed(steps: int, gather: bool, groups: int = 1):
         """K steps bracketed by a barrier + synchronise on both sides; max over ranks. HIP events on the
-        launch stream inside the same bracket give the kernel-stream time: the roofline's launch duration and,
-        in up to 20 consecutive groups, a per-step median / min / max (with the gather on, one group: the
-        gathers' stream waits would cut across group boundaries)."""
-        ngroups = max(1, min(20, steps)) if (pipe is None or not gather) else 1
+        launch stream inside the same bracket give the kernel-stream time (the roofline's launch duration);
+        with groups > 1, per-group events give a per-step median / min / max (not with the gather on: its
+        stream waits would cut across group boundaries)."""
+        ngroups = max(1, min(groups, steps)) if (pipe is None or not gather) else 1
         gsteps = [steps * (i + 1) // ngroups - steps * i // ngroups for i in range(ngroups)]
         evs = [torch.cuda.Event(enable_timing=True) for _ in range(ngroups + 1)]
         if multi:
@@ -572,10 +572,13 @@ def main():
     run_steps(args.warmup, True)
     torch.cuda.synchronize()
 
-    elapsed, kern_ms, per_step = timed(args.steps, gather=True)
+    # the timed region carries two events only (an event between two launches is a marker in the queue)
+    elapsed, kern_ms, _ = timed(args.steps, gather=True)
     compute_only = None
     if multi:  # the same steps without the gather: value_compute_only, and the roofline's kernel time
-        compute_only, kern_ms, per_step = timed(args.steps, gather=False)
+        compute_only, kern_ms, _ = timed(args.steps, gather=False)
+    # per-step spread: the same number of steps again, events around groups of steps (up to 20 groups)
+    _, _, per_step = timed(args.steps, gather=False, groups=20)
     kern_median = float(np.median(per_step))
     ngroups = len(per_step)
 
@@ -598,7 +601,8 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            # kernel-stream time per step (HIP events, no gather) over consecutive groups of steps
+            # kernel-stream time per step (HIP events, no gather) over up to 20 consecutive groups of steps, in a
+            # pass of its own right after the timed region
             "ms_per_step_median": round(kern_median, 4),
             "ms_per_step_min": round(per_step[0], 4),
             "ms_per_step_max": round(per_step[-1], 4),
