@@ -504,9 +504,13 @@ __global__ __launch_bounds__(kBlock) void crc32_arena_lines_kernel(const uint8_t
   arena_line_pass<PROBE>(base, ar, blockIdx.x, gridDim.x, lds4, img_slice, img_group8, img_sb);
 }
 
-// Extent of a variable batch (crc32_kernels.h launch_extent): grid-stride partials per block, the last
-// block to finish reduces them, resets the arrival counter for the stream's next call and publishes.
-// ws layout (uint64): [0] arrival counter, [1..4] result {lo, hi, sum, bad}, [8 + 4b ...] block b's partial.
+// Extent of a variable batch (crc32_kernels.h launch_extent), two launches and no fences: every block
+// writes its partial {lo, hi, sum, bad} with plain stores; a one-block launch after it (the kernel boundary
+// orders them) reduces the partials, writes the result for this call's arena launches and publishes it to
+// the pinned host record with relaxed system-scope stores plus a check word over the fields, which is how
+// the host tells a complete record from a torn one (a release at system scope would write back every dirty
+// L2 line of the preceding launches first).
+// ws layout (uint64): [1..4] result {lo, hi, sum, bad}, [8 + 4b ...] block b's partial.
 constexpr int kExtentBlock = 256;
 constexpr uint32_t kExtentMaxBlocks = (kExtentScratchBytes / 8 - 8) / 4;
 __device__ __forceinline__ uint64_t wave_min(uint64_t v) {
@@ -524,25 +528,9 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
   for (int d = 32; d >= 1; d >>= 1) v += (uint64_t)__shfl_xor((unsigned long long)v, d);
   return v;
 }
-
-__global__ __launch_bounds__(kExtentBlock) void crc32_extent_kernel(const uint64_t* __restrict__ off,
-                                                                    const uint32_t* __restrict__ len, size_t n,
-                                                                    uint64_t* ws, ExtentHint* host, uint64_t seq) {
+// {lo, hi, sum, bad} of this thread's values, reduced over the block into out[0..3] by thread 0
+__device__ __forceinline__ void block_reduce4(uint64_t lo, uint64_t hi, uint64_t sum, uint64_t bad, uint64_t* out) {
   __shared__ uint64_t red[4][kExtentBlock / 64];
-  __shared__ bool last;
-  uint64_t lo = ~0ull, hi = 0, sum = 0, bad = 0;
-  for (size_t i = blockIdx.x * (size_t)kExtentBlock + threadIdx.x; i < n; i += (size_t)gridDim.x * kExtentBlock) {
-    const uint64_t o = off[i], l = len[i];
-    if (l) {
-      lo = min(lo, o);
-      hi = max(hi, o + l);
-      sum += l;
-    }
-    if (i + 1 < n) {
-      const uint64_t o2 = off[i + 1];
-      bad |= (o2 < o || o2 - (o + l) >= 4096 && o2 >= o + l) ? 1u : 0u;
-    }
-  }
   lo = wave_min(lo);
   hi = wave_max(hi);
   sum = wave_sum(sum);
@@ -562,54 +550,52 @@ __global__ __launch_bounds__(kExtentBlock) void crc32_extent_kernel(const uint64
       sum += red[2][k];
       bad = max(bad, red[3][k]);
     }
-    uint64_t* part = ws + 8 + 4 * (size_t)blockIdx.x;
-    part[0] = lo;
-    part[1] = hi;
-    part[2] = sum;
-    part[3] = bad;
-    __threadfence();
-    last = atomicAdd(reinterpret_cast<unsigned long long*>(ws), 1ull) == gridDim.x - 1;
+    out[0] = lo;
+    out[1] = hi;
+    out[2] = sum;
+    out[3] = bad;
   }
-  __syncthreads();  // also: thread 0 is done reading red
-  if (!last) return;
-  // the last block: every partial is published (each block fenced before arriving)
-  __threadfence();
-  lo = ~0ull, hi = 0, sum = 0, bad = 0;
-  for (uint32_t b = threadIdx.x; b < gridDim.x; b += kExtentBlock) {
-    const volatile uint64_t* part = ws + 8 + 4 * (size_t)b;
-    lo = min(lo, (uint64_t)part[0]);
-    hi = max(hi, (uint64_t)part[1]);
-    sum += part[2];
-    bad = max(bad, (uint64_t)part[3]);
-  }
-  lo = wave_min(lo);
-  hi = wave_max(hi);
-  sum = wave_sum(sum);
-  bad = wave_max(bad);
-  if ((threadIdx.x & 63) == 0) {
-    red[0][w] = lo;
-    red[1][w] = hi;
-    red[2][w] = sum;
-    red[3][w] = bad;
-  }
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    for (int k = 1; k < kExtentBlock / 64; k++) {
-      lo = min(lo, red[0][k]);
-      hi = max(hi, red[1][k]);
-      sum += red[2][k];
-      bad = max(bad, red[3][k]);
+}
+
+__global__ __launch_bounds__(kExtentBlock) void crc32_extent_kernel(const uint64_t* __restrict__ off,
+                                                                    const uint32_t* __restrict__ len, size_t n,
+                                                                    uint64_t* ws) {
+  uint64_t lo = ~0ull, hi = 0, sum = 0, bad = 0;
+  for (size_t i = blockIdx.x * (size_t)kExtentBlock + threadIdx.x; i < n; i += (size_t)gridDim.x * kExtentBlock) {
+    const uint64_t o = off[i], l = len[i];
+    if (l) {
+      lo = min(lo, o);
+      hi = max(hi, o + l);
+      sum += l;
     }
-    ws[1] = lo;
-    ws[2] = hi;
-    ws[3] = sum;
-    ws[4] = bad;
-    ws[0] = 0;  // the arrival counter, for this stream's next call
-    host->lo = lo;
-    host->hi = hi;
-    host->sum = sum;
-    host->bad = bad;
-    __hip_atomic_store(&host->seq, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    if (i + 1 < n) {
+      const uint64_t o2 = off[i + 1];
+      bad |= (o2 < o || (o2 >= o + l && o2 - (o + l) >= 4096)) ? 1u : 0u;
+    }
+  }
+  block_reduce4(lo, hi, sum, bad, ws + 8 + 4 * (size_t)blockIdx.x);
+}
+
+__global__ __launch_bounds__(kExtentBlock) void crc32_extent_final_kernel(uint64_t* ws, uint32_t parts,
+                                                                          ExtentHint* host, uint64_t seq) {
+  uint64_t lo = ~0ull, hi = 0, sum = 0, bad = 0;
+  for (uint32_t b = threadIdx.x; b < parts; b += kExtentBlock) {
+    const uint64_t* part = ws + 8 + 4 * (size_t)b;
+    lo = min(lo, part[0]);
+    hi = max(hi, part[1]);
+    sum += part[2];
+    bad = max(bad, part[3]);
+  }
+  block_reduce4(lo, hi, sum, bad, ws + 1);
+  if (threadIdx.x == 0) {
+    lo = ws[1];
+    hi = ws[2];
+    sum = ws[3];
+    bad = ws[4];
+    const uint64_t f[6] = {lo, hi, sum, bad, seq, lo ^ hi ^ sum ^ bad ^ seq ^ kExtentCheck};
+    uint64_t* h = reinterpret_cast<uint64_t*>(host);
+#pragma unroll
+    for (int i = 0; i < 6; i++) __hip_atomic_store(h + i, f[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
 }
 
@@ -620,7 +606,11 @@ hipError_t launch_extent(const uint64_t* off, const uint32_t* len, size_t n, voi
   size_t blocks = (n + 4 * kExtentBlock - 1) / (4 * kExtentBlock);
   blocks = std::max<size_t>(1, std::min<size_t>({blocks, max_blocks, (size_t)kExtentMaxBlocks}));
   hipLaunchKernelGGL(crc32_extent_kernel, dim3((unsigned)blocks), dim3(kExtentBlock), 0, stream, off, len, n,
-                     static_cast<uint64_t*>(ws), host, seq);
+                     static_cast<uint64_t*>(ws));
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(crc32_extent_final_kernel, dim3(1), dim3(kExtentBlock), 0, stream, static_cast<uint64_t*>(ws),
+                     (uint32_t)blocks, host, seq);
   return hipGetLastError();
 }
 
@@ -729,16 +719,13 @@ hipError_t launch_arena(const ArenaLaunch& a, hipStream_t stream) {
   // The stitch issues a lane's next payload loads before folding the current one (PIPE 1): config-3 step
   // 0.2139-0.2142 ms vs 0.2144-0.2151 without, same box, three alternating pairs
   // (profiles/r02/stitch_pipe_bench_ab/). ANNETY_CRC_STITCH_PIPE=0 selects the one-payload-at-a-time loop.
-  // ANNETY_CRC_STITCH_BLK=768 (A/B): 768-lane blocks, one payload in flight per lane (PIPE 0) under the
-  // 168-VGPR cap of 3 waves per SIMD, instead of 512 lanes with two payloads in flight per lane.
-  static const int mode = [] {
+  // 768-lane blocks with one payload in flight (3 waves per SIMD under a 168-VGPR cap, no spill) measured
+  // 21.3 us against 20.4 for this 512-lane form (profiles/r03/stitch_ab/): occupancy is not what bounds it.
+  static const bool pipe = [] {
     const char* e = std::getenv("ANNETY_CRC_STITCH_PIPE");
-    const char* b = std::getenv("ANNETY_CRC_STITCH_BLK");
-    if (b && std::atoi(b) == 768) return 2;
-    return (e && e[0] == '0') ? 0 : 1;
+    return !(e && e[0] == '0');
   }();
-  if (mode == 2) return launch_stitch_p<0, 0, 768>(a, stream);
-  return mode == 1 ? launch_stitch_p<0, 1>(a, stream) : launch_stitch_p<0>(a, stream);
+  return pipe ? launch_stitch_p<0, 1>(a, stream) : launch_stitch_p<0>(a, stream);
 }
 
 }  // namespace annety_crc

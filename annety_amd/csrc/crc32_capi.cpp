@@ -331,8 +331,8 @@ struct DeviceCtx {
     uint64_t tick = 0;           // last use, for LRU hand-over
     hipEvent_t fence = nullptr;  // recorded on `last` only when the slot is handed to another stream
                                  // (per-thread handles: after every call, see scratch_done)
-    // automatic variable-path choice (run_var_auto): the extent kernel's area is the slot's first
-    // kExtentScratchBytes (its arrival counter zeroed when the slot is allocated); the paths' scratch follows
+    // automatic variable-path choice (run_var_auto): the extent kernels' area is the slot's first
+    // kExtentScratchBytes; the paths' scratch follows
     ExtentHint* hint = nullptr;  // pinned: the extent of this slot's latest completed auto call
     uint64_t calls = 0;          // extent kernels launched from this slot (hint->seq numbers them)
     struct Key {
@@ -564,7 +564,6 @@ int scratch_slot(DeviceCtx& c, hipStream_t stream, size_t bytes, DeviceCtx::Scra
     slot->ptr = nullptr;
     slot->bytes = 0;
     HIP_TRY(hipMallocAsync(&slot->ptr, kExtentScratchBytes + bytes, stream));
-    HIP_TRY(hipMemsetAsync(slot->ptr, 0, 8, stream));  // the extent kernel's arrival counter
     slot->bytes = bytes;
   }
   slot->last = stream;
@@ -699,15 +698,16 @@ constexpr size_t kAutoMinPayloads = 1024;  // below this the extent kernel is no
 
 // Reads the slot's pinned record; true if a new completed one for the current key arrived.
 bool poll_hint(DeviceCtx::ScratchSlot* s) {
-  const uint64_t seq = __atomic_load_n(&s->hint->seq, __ATOMIC_ACQUIRE);
-  if (seq <= s->seen_seq || seq < s->key_since) return false;
   ExtentHint h{};
-  h.lo = s->hint->lo;
-  h.hi = s->hint->hi;
-  h.sum = s->hint->sum;
-  h.bad = s->hint->bad;
-  if (__atomic_load_n(&s->hint->seq, __ATOMIC_ACQUIRE) != seq) return false;  // rewritten meanwhile: next call
-  h.seq = seq;
+  h.lo = __atomic_load_n(&s->hint->lo, __ATOMIC_RELAXED);
+  h.hi = __atomic_load_n(&s->hint->hi, __ATOMIC_RELAXED);
+  h.sum = __atomic_load_n(&s->hint->sum, __ATOMIC_RELAXED);
+  h.bad = __atomic_load_n(&s->hint->bad, __ATOMIC_RELAXED);
+  h.seq = __atomic_load_n(&s->hint->seq, __ATOMIC_RELAXED);
+  h.chk = __atomic_load_n(&s->hint->chk, __ATOMIC_RELAXED);
+  if ((h.lo ^ h.hi ^ h.sum ^ h.bad ^ h.seq ^ kExtentCheck) != h.chk) return false;  // torn: the next call reads it
+  const uint64_t seq = h.seq;
+  if (seq <= s->seen_seq || seq < s->key_since) return false;
   if (s->seen_seq >= s->key_since) {
     s->prev = s->seen;
     s->prev_seq = s->seen_seq;

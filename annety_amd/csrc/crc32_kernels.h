@@ -98,12 +98,14 @@ struct ArenaLaunch {
 // non-empty payloads lo = min offset, hi = max end, sum = total bytes; bad != 0 unless every payload starts
 // at or after the previous one and within 4 KiB of its end (then every byte of [lo, hi) lies on a page that
 // also holds payload bytes, so the arena path reads only mapped memory). ExtentResult = {lo, hi, sum, bad}.
-// Written to the device scratch `ws` (kExtentScratchBytes, its counter zeroed once when allocated) and,
-// with `seq` last (release, system scope), to the pinned host record `host` (ExtentHint).
+// Written to the device scratch `ws` (kExtentScratchBytes) and to the pinned host record `host`
+// (ExtentHint), whose `chk` = lo ^ hi ^ sum ^ bad ^ seq ^ kExtentCheck lets the host reject a record it read
+// while the device was rewriting it.
 constexpr size_t kExtentScratchBytes = 16384;
+constexpr uint64_t kExtentCheck = 0x9E3779B97F4A7C15ull;
 struct ExtentHint {
   uint64_t lo, hi, sum, bad;
-  uint64_t seq;
+  uint64_t seq, chk;
 };
 hipError_t launch_extent(const uint64_t* off, const uint32_t* len, size_t n, void* ws, ExtentHint* host,
                          uint64_t seq, size_t max_blocks, hipStream_t stream);
