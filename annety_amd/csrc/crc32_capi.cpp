@@ -38,7 +38,10 @@ int hip_fail(hipError_t e) {
 
 // ---------------- host worker pool (staging packs) ----------------
 // Pageable -> pinned packing is a host memcpy; one thread moves ~10-20 GB/s, below PCIe Gen5 x16, so the
-// pack is split over a small persistent pool (ANNETY_CRC_PACK_THREADS, default min(8, cores)).
+// pack is split over a small persistent pool (ANNETY_CRC_PACK_THREADS, default min(8, cores)). Several
+// callers may pack at once (the device group's per-device threads, concurrent host batches): each run() is
+// a job in a shared list, the workers take pieces of any job, and every caller also works on its own job
+// until it is done, so concurrent packs share the workers instead of queueing behind one another.
 class PackPool {
  public:
   static PackPool& get() {
@@ -54,24 +57,36 @@ class PackPool {
       for (size_t i = 0; i < n; i++) fn(i);
       return;
     }
-    std::unique_lock<std::mutex> one(run_mu_);  // one parallel region at a time
+    Job job;
     std::function<void(size_t)> f = fn;
+    job.fn = &f;
+    job.total = job.left = n;
     {
       std::lock_guard<std::mutex> lk(mu_);
-      job_ = &f;
-      next_ = 0;
-      total_ = n;
-      left_ = n;
-      gen_++;
+      jobs_.push_back(&job);
     }
     cv_.notify_all();
-    work();
+    for (;;) {  // the caller works on its own job
+      size_t i;
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (job.next >= job.total) break;
+        i = job.next++;
+      }
+      f(i);
+      finish(job);
+    }
     std::unique_lock<std::mutex> lk(mu_);
-    done_cv_.wait(lk, [&] { return left_ == 0; });
-    job_ = nullptr;
+    job.done_cv.wait(lk, [&] { return job.left == 0; });
+    jobs_.erase(std::find(jobs_.begin(), jobs_.end(), &job));
   }
 
  private:
+  struct Job {
+    std::function<void(size_t)>* fn = nullptr;
+    size_t next = 0, total = 0, left = 0;
+    std::condition_variable done_cv;
+  };
   PackPool() {
     int t = (int)std::min<unsigned>(8, std::max<unsigned>(1, std::thread::hardware_concurrency()));
     if (const char* e = std::getenv("ANNETY_CRC_PACK_THREADS")) t = std::max(1, std::min(64, std::atoi(e)));
@@ -85,39 +100,38 @@ class PackPool {
     cv_.notify_all();
     for (auto& w : workers_) w.join();
   }
-  void work() {
-    for (;;) {
-      size_t i;
-      std::function<void(size_t)>* f;
-      {
-        std::lock_guard<std::mutex> lk(mu_);
-        if (!job_ || next_ >= total_) return;
-        i = next_++;
-        f = job_;
-      }
-      (*f)(i);
-      std::lock_guard<std::mutex> lk(mu_);
-      if (--left_ == 0) done_cv_.notify_all();
-    }
+  void finish(Job& job) {
+    std::lock_guard<std::mutex> lk(mu_);
+    if (--job.left == 0) job.done_cv.notify_all();
   }
   void loop() {
-    uint64_t seen = 0;
     for (;;) {
+      Job* job = nullptr;
+      size_t i = 0;
       {
         std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+        cv_.wait(lk, [&] {
+          if (stop_) return true;
+          for (Job* j : jobs_)
+            if (j->next < j->total) return true;
+          return false;
+        });
         if (stop_) return;
-        seen = gen_;
+        for (Job* j : jobs_)
+          if (j->next < j->total) {
+            job = j;
+            break;
+          }
+        i = job->next++;
       }
-      work();
+      (*job->fn)(i);
+      finish(*job);
     }
   }
   std::vector<std::thread> workers_;
-  std::mutex mu_, run_mu_;
-  std::condition_variable cv_, done_cv_;
-  std::function<void(size_t)>* job_ = nullptr;
-  size_t next_ = 0, total_ = 0, left_ = 0;
-  uint64_t gen_ = 0;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  std::vector<Job*> jobs_;  // jobs with pieces left or still being finished (owned by their callers)
   bool stop_ = false;
 };
 
