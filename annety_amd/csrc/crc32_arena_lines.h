@@ -16,12 +16,37 @@ struct LineOut {
   uint64_t byte_lo, byte_hi, line_lo, line_hi, sb0, nsb, fs0, fs1;
   uint64_t zero_line;
   const uint64_t* check;  // ArenaLaunch::check
+  uint32_t check_parts;
   uint64_t check_lo, check_hi;
 };
 
-// ArenaLaunch::check: this call's extent (ExtentResult) equals the declared one and the batch is safe.
-__device__ __forceinline__ bool extent_matches(const uint64_t* check, uint64_t lo, uint64_t hi) {
-  return !check || (check[0] == lo && check[1] == hi && check[3] == 0);
+// This call's extent from the launch_extent partials (ws + 8 + 4b: {lo, hi, sum, bad} of block b), reduced
+// by the calling wave; every wave computes the same values.
+__device__ __forceinline__ void extent_of(const uint64_t* ws, uint32_t parts, uint64_t& lo, uint64_t& hi,
+                                          uint64_t& sum, uint64_t& bad) {
+  lo = ~0ull;
+  hi = sum = bad = 0;
+  for (uint32_t b = threadIdx.x & 63; b < parts; b += 64) {
+    const uint64_t* q = ws + 8 + 4 * (size_t)b;
+    lo = min(lo, q[0]);
+    hi = max(hi, q[1]);
+    sum += q[2];
+    bad |= q[3];
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    lo = min(lo, (uint64_t)__shfl_xor((unsigned long long)lo, d));
+    hi = max(hi, (uint64_t)__shfl_xor((unsigned long long)hi, d));
+    sum += (uint64_t)__shfl_xor((unsigned long long)sum, d);
+    bad |= (uint64_t)__shfl_xor((unsigned long long)bad, d);
+  }
+}
+// ArenaLaunch::check: this call's extent equals the declared one and the batch is safe.
+__device__ __forceinline__ bool extent_matches(const uint64_t* check, uint32_t parts, uint64_t lo, uint64_t hi) {
+  if (!check) return true;
+  uint64_t l, h, s, b;
+  extent_of(check, parts, l, h, s, b);
+  return l == lo && h == hi && b == 0;
 }
 
 //   PROBE (microbench only; product = 0): bit 0 drops the S stores, bit 1 the superblock scan - wrong
@@ -41,7 +66,8 @@ __device__ __forceinline__ void arena_line_pass(const uint8_t* __restrict__ base
                                                 const uint4* __restrict__ img_group8,
                                                 const uint4* __restrict__ img_sb) {
   constexpr int BLK = kBlock, VWG = kVwg;
-  if (!extent_matches(ar.check, ar.check_lo, ar.check_hi)) return;  // uniform over the grid: the stitch folds directly
+  // uniform over the grid: on a mismatch the stitch folds every payload directly
+  if (!extent_matches(ar.check, ar.check_parts, ar.check_lo, ar.check_hi)) return;
   const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
   const uint32_t j = threadIdx.x & 7;
   const size_t gid = (((size_t)bid + (size_t)nbid * (threadIdx.x / VWG)) * VWG + threadIdx.x % VWG) / 8;

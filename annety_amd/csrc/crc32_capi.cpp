@@ -766,18 +766,23 @@ int run_var_auto(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_o
     a.check_hi = h.hi;
     if (a.nsb && (rc = scratch_slot(c, stream, arena_geom(a).words * sizeof(uint32_t), &slot))) return rc;
   }
-  // this call's extent: the next calls' record, and the check the arena launches make
+  // this call's extent: the check the arena launches make, and the next calls' record
   const uint64_t seq = ++slot->calls;
-  hipError_t e = launch_extent(d_off, d_len, n, slot->ptr, slot->hint, seq, grid_cus(c), stream);
+  uint32_t parts = 0;
+  hipError_t e = launch_extent(d_off, d_len, n, slot->ptr, grid_cus(c), &parts, stream);
   if (e != hipSuccess) return hip_fail(e);
   (arena ? c.auto_arena : c.auto_sorted)++;
   if (arena) {
-    a.check = extent_result(slot->ptr);
+    a.check = static_cast<const uint64_t*>(slot->ptr);
+    a.check_parts = parts;
+    a.record = slot->hint;
+    a.record_seq = seq;
     a.scratch = reinterpret_cast<uint32_t*>(path_scratch(slot));
     e = launch_arena(a, stream);
     rc = e == hipSuccess ? ANNETY_CRC_OK : hip_fail(e);
   } else {
-    rc = run_var_sorted_in(c, slot, d_base, n, d_off, d_len, d_out, stream, update);
+    e = launch_extent_publish(slot->ptr, parts, slot->hint, seq, stream);
+    rc = e == hipSuccess ? run_var_sorted_in(c, slot, d_base, n, d_off, d_len, d_out, stream, update) : hip_fail(e);
   }
   const int rd = scratch_done(slot, stream);
   return rc ? rc : rd;

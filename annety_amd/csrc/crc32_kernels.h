@@ -65,6 +65,19 @@ hipError_t launch_split_desc(const void* base, size_t n, uint64_t len, uint64_t 
 hipError_t launch_split_join(const uint32_t* seg_crc, size_t n, uint32_t S, const uint32_t* powers, uint32_t* out,
                              hipStream_t stream);
 
+// Extent of a variable batch, for the automatic choice between the arena and the sorted path: over the
+// non-empty payloads lo = min offset, hi = max end, sum = total bytes; bad != 0 unless every payload starts
+// at or after the previous one and within 4 KiB of its end (then every byte of [lo, hi) lies on a page that
+// also holds payload bytes, so the arena path reads only mapped memory). ExtentResult = {lo, hi, sum, bad}.
+// Written to the device scratch `ws` (kExtentScratchBytes) and to the pinned host record `host`
+// (ExtentHint), whose `chk` = lo ^ hi ^ sum ^ bad ^ seq ^ kExtentCheck lets the host reject a record it read
+// while the device was rewriting it.
+constexpr size_t kExtentScratchBytes = 16384;
+constexpr uint64_t kExtentCheck = 0x9E3779B97F4A7C15ull;
+struct ExtentHint {
+  uint64_t lo, hi, sum, bad;
+  uint64_t seq, chk;
+};
 // Arena path (crc32_arena.hip): bulk line pass over the arena [byte_lo, byte_hi) (absolute 128-byte
 // lines line_lo..line_hi, superblocks of 64 lines from sb0, nsb of them; nsb = 0 skips the pass), then
 // the per-payload stitch. DESIGN.md §2.8.
@@ -87,29 +100,22 @@ struct ArenaLaunch {
   size_t max_blocks;
   bool update;
   // automatic path selection (annety_crc32_batch_var): the arena was declared from an earlier call's
-  // extent; both launches check this call's extent (ExtentResult, written by launch_extent on the same
-  // stream) against [check_lo, check_hi) first - on any difference the line pass does nothing and every
-  // payload is folded directly from its own bytes (no read outside the payloads). null = no check.
+  // extent; both launches first reduce this call's extent from the launch_extent partials (check,
+  // check_parts; same stream) and compare it with [check_lo, check_hi) - on any difference the line pass
+  // does nothing and every payload is folded directly from its own bytes (no read outside the payloads).
+  // The stitch also publishes the reduced extent to `record` (seq = record_seq). null = no check.
   const uint64_t* check;
+  uint32_t check_parts;
   uint64_t check_lo, check_hi;
+  ExtentHint* record;
+  uint64_t record_seq;
 };
 
-// Extent of a variable batch, for the automatic choice between the arena and the sorted path: over the
-// non-empty payloads lo = min offset, hi = max end, sum = total bytes; bad != 0 unless every payload starts
-// at or after the previous one and within 4 KiB of its end (then every byte of [lo, hi) lies on a page that
-// also holds payload bytes, so the arena path reads only mapped memory). ExtentResult = {lo, hi, sum, bad}.
-// Written to the device scratch `ws` (kExtentScratchBytes) and to the pinned host record `host`
-// (ExtentHint), whose `chk` = lo ^ hi ^ sum ^ bad ^ seq ^ kExtentCheck lets the host reject a record it read
-// while the device was rewriting it.
-constexpr size_t kExtentScratchBytes = 16384;
-constexpr uint64_t kExtentCheck = 0x9E3779B97F4A7C15ull;
-struct ExtentHint {
-  uint64_t lo, hi, sum, bad;
-  uint64_t seq, chk;
-};
-hipError_t launch_extent(const uint64_t* off, const uint32_t* len, size_t n, void* ws, ExtentHint* host,
-                         uint64_t seq, size_t max_blocks, hipStream_t stream);
-inline const uint64_t* extent_result(const void* ws) { return static_cast<const uint64_t*>(ws) + 1; }
+// The per-block partials (returns their count in *parts); the arena launches reduce them themselves.
+hipError_t launch_extent(const uint64_t* off, const uint32_t* len, size_t n, void* ws, size_t max_blocks,
+                         uint32_t* parts, hipStream_t stream);
+// One block reducing the partials and publishing them to `host` (the sorted path, which has no stitch).
+hipError_t launch_extent_publish(const void* ws, uint32_t parts, ExtentHint* host, uint64_t seq, hipStream_t stream);
 
 // Line-pass layout. L line-pass workgroups of 512 lanes = W = 8L waves = 64L lane groups;
 // wave w's task t is full superblock fs0 + t*W + w (lane group g = 8w + block). Per line of a full
