@@ -528,8 +528,11 @@ __global__ __launch_bounds__(kBlock) void crc32_arena_lines_kernel(const uint8_t
 // last block to arrive, behind device-scope fences, and published with a system-scope release: 11.4 us per
 // call, every release writing back the dirty L2 lines of the launches before it.)
 // ws layout (uint64): [8 + 4b ...] block b's partial.
-constexpr int kExtentBlock = 256;
-constexpr uint32_t kExtentMaxBlocks = (kExtentScratchBytes / 8 - 8) / 4;
+// At most kExtentMaxParts partials: every block of the line pass and of the stitch reduces them all (510
+// partials of 256-thread blocks cost the config-3 line pass 3.5 us and the stitch 3.6).
+constexpr int kExtentBlock = 1024;
+constexpr uint32_t kExtentMaxParts = 128;
+static_assert(8 + 4 * kExtentMaxParts <= kExtentScratchBytes / 8, "extent partials exceed the scratch");
 __device__ __forceinline__ uint64_t wave_min(uint64_t v) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v = min(v, (uint64_t)__shfl_xor((unsigned long long)v, d));
@@ -609,9 +612,9 @@ __global__ __launch_bounds__(64) void crc32_extent_publish_kernel(const uint64_t
 
 hipError_t launch_extent(const uint64_t* off, const uint32_t* len, size_t n, void* ws, size_t max_blocks,
                          uint32_t* parts, hipStream_t stream) {
-  // about one payload per thread, up to the partials the scratch holds: the launch is latency-bound
+  // about one payload per thread (the launch is latency-bound), up to kExtentMaxParts partials
   size_t blocks = (n + kExtentBlock - 1) / kExtentBlock;
-  blocks = std::max<size_t>(1, std::min<size_t>({blocks, 2 * max_blocks, (size_t)kExtentMaxBlocks}));
+  blocks = std::max<size_t>(1, std::min<size_t>({blocks, 2 * max_blocks, (size_t)kExtentMaxParts}));
   *parts = (uint32_t)blocks;
   hipLaunchKernelGGL(crc32_extent_kernel, dim3((unsigned)blocks), dim3(kExtentBlock), 0, stream, off, len, n,
                      static_cast<uint64_t*>(ws));

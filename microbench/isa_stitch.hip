@@ -14,3 +14,10 @@ void* isa_stitch_kernels[] = {
     reinterpret_cast<void*>(&crc32_arena_stitch_kernel<true, 1024, 0, 1>),
 };
 }  // namespace annety_crc
+namespace annety_crc {
+void* isa_stitch_lite_kernels[] = {
+    reinterpret_cast<void*>(&crc32_arena_stitch_lite_kernel<false, 256, 4>),
+    reinterpret_cast<void*>(&crc32_arena_stitch_lite_kernel<false, 512, 4>),
+    reinterpret_cast<void*>(&crc32_arena_stitch_lite_kernel<false, 256, 3>),
+};
+}  // namespace annety_crc
