@@ -391,6 +391,15 @@ __device__ __forceinline__ LaneCtx lane_ctx() {
   return k;
 }
 
+// Relaxed system-scope stores of the extent record and its check word (crc32_kernels.h ExtentHint).
+__device__ __forceinline__ void publish_extent(ExtentHint* host, uint64_t lo, uint64_t hi, uint64_t sum, uint64_t bad,
+                                               uint64_t seq) {
+  const uint64_t f[6] = {lo, hi, sum, bad, seq, lo ^ hi ^ sum ^ bad ^ seq ^ kExtentCheck};
+  uint64_t* h = reinterpret_cast<uint64_t*>(host);
+#pragma unroll
+  for (int i = 0; i < 6; i++) __hip_atomic_store(h + i, f[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Second launch of the two-launch path: contiguous payload ranges per block (coalesced descriptor loads),
 // the same count for every block; the first payload's loads are in flight while the LDS image is staged.
 //   PIPE (microbench A/B, product = 0): 1 = the next payload's loads are issued before the
@@ -406,12 +415,8 @@ __global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchGeo g0, c
     uint64_t lo, hi, sum, bad;
     extent_of(g.check, g.check_parts, lo, hi, sum, bad);
     if (!(lo == g.check_lo && hi == g.check_hi && bad == 0)) g.byte_lo = g.byte_hi = 0;
-    if (blockIdx.x == 0 && threadIdx.x == 0 && g.record) {  // the next calls' record (crc32_kernels.h)
-      const uint64_t f[6] = {lo, hi, sum, bad, g.record_seq, lo ^ hi ^ sum ^ bad ^ g.record_seq ^ kExtentCheck};
-      uint64_t* h = reinterpret_cast<uint64_t*>(g.record);
-#pragma unroll
-      for (int i = 0; i < 6; i++) __hip_atomic_store(h + i, f[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && g.record)  // the next calls' record (crc32_kernels.h)
+      publish_extent(g.record, lo, hi, sum, bad, g.record_seq);
   }
   const Stitcher<UPD, PROBE> st{g, reinterpret_cast<const uint32_t*>(lds4), lane_ctx()};
   const size_t per = (g.n + gridDim.x - 1) / gridDim.x;
@@ -522,17 +527,15 @@ __global__ __launch_bounds__(kBlock) void crc32_arena_lines_kernel(const uint8_t
 // Extent of a variable batch (crc32_kernels.h launch_extent), no fences: every block writes its partial
 // {lo, hi, sum, bad} with plain stores; the next launches on the stream (the kernel boundary orders them)
 // reduce the partials themselves, one wave at a time (extent_of): the line pass and the stitch check the
-// declared arena against them, and the stitch (or, on the sorted path, crc32_extent_publish_kernel)
-// publishes the result to the pinned host record with relaxed system-scope stores plus a check word over
-// the fields, which is how the host tells a complete record from a torn one. (A first version reduced in the
-// last block to arrive, behind device-scope fences, and published with a system-scope release: 11.4 us per
-// call, every release writing back the dirty L2 lines of the launches before it.)
-// ws layout (uint64): [8 + 4b ...] block b's partial.
-// At most kExtentMaxParts partials: every block of the line pass and of the stitch reduces them all (510
-// partials of 256-thread blocks cost the config-3 line pass 3.5 us and the stitch 3.6).
-constexpr int kExtentBlock = 1024;
-constexpr uint32_t kExtentMaxParts = 128;
-static_assert(8 + 4 * kExtentMaxParts <= kExtentScratchBytes / 8, "extent partials exceed the scratch");
+// declared arena against them, and the stitch (or, on the sorted path, crc32_bucket_place) publishes the
+// result to the pinned host record with relaxed system-scope stores plus a check word over the fields,
+// which is how the host tells a complete record from a torn one. (A first version reduced in the last
+// block to arrive, behind device-scope fences, and published with a system-scope release: 11.4 us per
+// call, every release writing back the dirty L2 lines of the launches before it.) At most kExtentMaxParts
+// partials: every block of the line pass and of the stitch reduces them all (510 partials of 256-thread
+// blocks cost the config-3 line pass 3.5 us and the stitch 3.6).
+// ws layout (uint64): [8 + 4b ...] block b's partial; bytes [kCursorOff, +8 KiB) the bucket cursors.
+constexpr int kExtentBlock = kBucketThreads;
 __device__ __forceinline__ uint64_t wave_min(uint64_t v) {
 #pragma unroll
   for (int d = 32; d >= 1; d >>= 1) v = min(v, (uint64_t)__shfl_xor((unsigned long long)v, d));
@@ -577,9 +580,22 @@ __device__ __forceinline__ void block_reduce4(uint64_t lo, uint64_t hi, uint64_t
   }
 }
 
+// Bucket of a non-empty payload at absolute address a: 1023 - its 128-byte line count (longest first).
+__device__ __forceinline__ uint32_t bucket_of(uint64_t a, uint32_t len) {
+  const uint32_t nl = (uint32_t)(((a + len - 1) >> 7) - (a >> 7) + 1);
+  return (kBucketCount - 1) - (nl < kBucketCount - 1 ? nl : kBucketCount - 1);
+}
+
+// COUNT: step 1 of the counting sort (crc32_kernels.h BucketArgs) beside the extent.
+template <bool COUNT>
 __global__ __launch_bounds__(kExtentBlock) void crc32_extent_kernel(const uint64_t* __restrict__ off,
                                                                     const uint32_t* __restrict__ len, size_t n,
-                                                                    uint64_t* ws) {
+                                                                    uint64_t* ws, BucketArgs bk) {
+  __shared__ uint32_t h[COUNT ? kBucketCount : 1];
+  if constexpr (COUNT) {
+    for (uint32_t i = threadIdx.x; i < kBucketCount; i += kExtentBlock) h[i] = 0;
+    __syncthreads();
+  }
   uint64_t lo = ~0ull, hi = 0, sum = 0, bad = 0;
   for (size_t i = blockIdx.x * (size_t)kExtentBlock + threadIdx.x; i < n; i += (size_t)gridDim.x * kExtentBlock) {
     const uint64_t o = off[i], l = len[i];
@@ -592,38 +608,99 @@ __global__ __launch_bounds__(kExtentBlock) void crc32_extent_kernel(const uint64
       const uint64_t o2 = off[i + 1];
       bad |= (o2 < o || (o2 >= o + l && o2 - (o + l) >= 4096)) ? 1u : 0u;
     }
+    if constexpr (COUNT) {
+      if (l)
+        atomicAdd(&h[bucket_of((uint64_t)(uintptr_t)bk.base + o, (uint32_t)l)], 1u);
+      else if (bk.out)
+        bk.out[i] = 0u;  // crc of the empty string (update mode: the register is unchanged)
+    }
   }
-  block_reduce4(lo, hi, sum, bad, ws + 8 + 4 * (size_t)blockIdx.x);
+  block_reduce4(lo, hi, sum, bad, ws + 8 + 4 * (size_t)blockIdx.x);  // (its barrier also orders h)
+  if constexpr (COUNT) {
+    __syncthreads();
+    uint32_t* row = bk.rows + (size_t)blockIdx.x * kBucketCount;
+    for (uint32_t i = threadIdx.x; i < kBucketCount; i += kExtentBlock) {
+      const uint32_t c = h[i];
+      if (c) row[i] = __hip_atomic_fetch_add(bk.cursor + i, c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
-__global__ __launch_bounds__(64) void crc32_extent_publish_kernel(const uint64_t* ws, uint32_t parts, ExtentHint* host,
-                                                                   uint64_t seq) {
-  uint64_t lo, hi, sum, bad;
-  extent_of(ws, parts, lo, hi, sum, bad);
-  if (threadIdx.x == 0) {
-    const uint64_t f[6] = {lo, hi, sum, bad, seq, lo ^ hi ^ sum ^ bad ^ seq ^ kExtentCheck};
-    uint64_t* h = reinterpret_cast<uint64_t*>(host);
+// Step 2 of the counting sort (crc32_kernels.h); the same grid and payload-to-block map as step 1.
+__global__ __launch_bounds__(kBucketThreads) void crc32_bucket_place(const uint64_t* __restrict__ off,
+                                                                     const uint32_t* __restrict__ len, size_t n,
+                                                                     const uint64_t* ws, uint32_t parts, BucketArgs bk,
+                                                                     ExtentHint* record, uint64_t seq) {
+  static_assert(kBucketThreads == kBucketCount, "one bucket per thread");
+  __shared__ uint32_t basep[kBucketCount];
+  __shared__ uint32_t wtot[kBucketThreads / 64];
+  const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+  // bucket totals (step 1's atomics, finished at the kernel boundary) -> exclusive bucket bases
+  const uint32_t tot = __hip_atomic_load(bk.cursor + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  const uint32_t mine = bk.rows[(size_t)blockIdx.x * kBucketCount + t];  // valid where this block has payloads
+  uint32_t v = tot;
 #pragma unroll
-    for (int i = 0; i < 6; i++) __hip_atomic_store(h + i, f[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  for (int d = 1; d < 64; d <<= 1) {
+    const uint32_t u = (uint32_t)__shfl_up((int)v, d);
+    if (lane >= (uint32_t)d) v += u;
+  }
+  if (lane == 63) wtot[w] = v;
+  __syncthreads();
+  uint32_t before = 0;
+  for (uint32_t k = 0; k < w; k++) before += wtot[k];
+  const uint32_t start = before + v - tot;
+  basep[t] = start + mine;
+  if (blockIdx.x == 0) {
+    bk.cursor_next[t] = 0u;
+    // classes by line count (bucket = 1023 - lines): >= 128 lines, 24..127, < 24, run at G = 32 / 16 / 4
+    // (crc32_capi.cpp run_var_sorted_in; on the config-3 batch the middle and small classes ran 12 % and
+    // 15 % faster at G = 16 / 4 than at 8 / 2: profiles/r02/ab4_stages.log)
+    constexpr uint32_t b16 = kBucketCount - 128, b4 = kBucketCount - 24;
+    if (t == 0) bk.ranges[0] = 0u;
+    if (t == b16) bk.ranges[1] = bk.ranges[2] = start;
+    if (t == b4) bk.ranges[3] = bk.ranges[4] = start;
+    if (t == kBucketCount - 1) bk.ranges[5] = start + tot;
+    if (record && w == 0) {
+      uint64_t lo, hi, sum, bad;
+      extent_of(ws, parts, lo, hi, sum, bad);
+      if (t == 0) publish_extent(record, lo, hi, sum, bad, seq);
+    }
+  }
+  __syncthreads();
+  uint4* desc = static_cast<uint4*>(bk.desc);
+  for (size_t i = blockIdx.x * (size_t)kBucketThreads + t; i < n; i += (size_t)gridDim.x * kBucketThreads) {
+    const uint32_t l = len[i];
+    if (!l) continue;
+    const uint64_t a = (uint64_t)(uintptr_t)bk.base + off[i];
+    const uint32_t pos = atomicAdd(&basep[bucket_of(a, l)], 1u);  // LDS atomic: rank inside the block's slots
+    desc[pos] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), l, (uint32_t)i);
   }
 }
 
 }  // namespace
 
-hipError_t launch_extent(const uint64_t* off, const uint32_t* len, size_t n, void* ws, size_t max_blocks,
-                         uint32_t* parts, hipStream_t stream) {
-  // about one payload per thread (the launch is latency-bound), up to kExtentMaxParts partials
-  size_t blocks = (n + kExtentBlock - 1) / kExtentBlock;
-  blocks = std::max<size_t>(1, std::min<size_t>({blocks, 2 * max_blocks, (size_t)kExtentMaxParts}));
-  *parts = (uint32_t)blocks;
-  hipLaunchKernelGGL(crc32_extent_kernel, dim3((unsigned)blocks), dim3(kExtentBlock), 0, stream, off, len, n,
-                     static_cast<uint64_t*>(ws));
+unsigned bucket_grid(size_t n) {
+  // about one payload per thread (the launches are latency-bound), up to kExtentMaxParts blocks
+  return (unsigned)std::max<size_t>(1, std::min<size_t>((n + kExtentBlock - 1) / kExtentBlock, kExtentMaxParts));
+}
+
+hipError_t launch_extent(const uint64_t* off, const uint32_t* len, size_t n, void* ws, uint32_t* parts,
+                         const BucketArgs* bk, hipStream_t stream) {
+  const unsigned blocks = bucket_grid(n);
+  *parts = blocks;
+  if (bk)
+    hipLaunchKernelGGL(crc32_extent_kernel<true>, dim3(blocks), dim3(kExtentBlock), 0, stream, off, len, n,
+                       static_cast<uint64_t*>(ws), *bk);
+  else
+    hipLaunchKernelGGL(crc32_extent_kernel<false>, dim3(blocks), dim3(kExtentBlock), 0, stream, off, len, n,
+                       static_cast<uint64_t*>(ws), BucketArgs{});
   return hipGetLastError();
 }
 
-hipError_t launch_extent_publish(const void* ws, uint32_t parts, ExtentHint* host, uint64_t seq, hipStream_t stream) {
-  hipLaunchKernelGGL(crc32_extent_publish_kernel, dim3(1), dim3(64), 0, stream, static_cast<const uint64_t*>(ws), parts,
-                     host, seq);
+hipError_t launch_bucket_place(const uint64_t* off, const uint32_t* len, size_t n, const void* ws, uint32_t parts,
+                               const BucketArgs& bk, ExtentHint* record, uint64_t seq, hipStream_t stream) {
+  hipLaunchKernelGGL(crc32_bucket_place, dim3(bucket_grid(n)), dim3(kBucketThreads), 0, stream, off, len, n,
+                     static_cast<const uint64_t*>(ws), parts, bk, record, seq);
   return hipGetLastError();
 }
 

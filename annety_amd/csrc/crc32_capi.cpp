@@ -349,6 +349,9 @@ struct DeviceCtx {
     // kExtentScratchBytes; the paths' scratch follows
     ExtentHint* hint = nullptr;  // pinned: the extent of this slot's latest completed auto call
     uint64_t calls = 0;          // extent kernels launched from this slot (hint->seq numbers them)
+    // the sorted path's bucket cursors (crc32_kernels.h BucketArgs): set (sorts & 1) is this call's
+    uint64_t sorts = 0;
+    bool cursors_clean = false;  // both sets zero (false after an allocation or a failed sort)
     struct Key {
       const void *base, *off, *len;
       size_t n;
@@ -579,6 +582,7 @@ int scratch_slot(DeviceCtx& c, hipStream_t stream, size_t bytes, DeviceCtx::Scra
     slot->bytes = 0;
     HIP_TRY(hipMallocAsync(&slot->ptr, kExtentScratchBytes + bytes, stream));
     slot->bytes = bytes;
+    slot->cursors_clean = false;
   }
   slot->last = stream;
   slot->tid = std::this_thread::get_id();
@@ -599,28 +603,49 @@ int scratch_done(DeviceCtx::ScratchSlot* slot, hipStream_t stream) {
   return r == hipSuccess ? ANNETY_CRC_OK : hip_fail(r);
 }
 
-// Variable batch: bucket by line count on the device (no host round trip), then one launch per
-// length class with its own lane-group width. Scratch: the stream's slot (scratch_slot).
+// Variable batch: counting sort by line count on the device (no host round trip; two launches,
+// crc32_kernels.h BucketArgs), then one launch per length class with its own lane-group width. Scratch:
+// the stream's slot (scratch_slot): the bucket cursors in the extent area, rows + ranges + descriptors
+// after it.
 size_t sorted_scratch_bytes(size_t n) {
-  const size_t rows_words = (size_t)bucket_blocks(n) * bucket_count();
+  const size_t rows_words = (size_t)bucket_grid(n) * kBucketCount;
   return (rows_words + 8) * sizeof(uint32_t) + 16 * n;  // rows + ranges (16-byte multiple) + descriptors
 }
 
-// The sorted path's launches into `slot` (sized by sorted_scratch_bytes; c.arena_mu held).
+// The sorted path's launches into `slot` (sized by sorted_scratch_bytes; c.arena_mu held). `record`
+// (automatic path): the extent record the bucket pass publishes, numbered `seq`.
 int run_var_sorted_in(DeviceCtx& c, DeviceCtx::ScratchSlot* slot, const void* d_base, size_t n, const uint64_t* d_off,
-                      const uint32_t* d_len, uint32_t* d_out, hipStream_t stream, bool update) {
-  const size_t rows_words = (size_t)bucket_blocks(n) * bucket_count();
-  const size_t head = (rows_words + 8) * sizeof(uint32_t);
-  int rc = ANNETY_CRC_OK;
+                      const uint32_t* d_len, uint32_t* d_out, hipStream_t stream, bool update,
+                      ExtentHint* record = nullptr, uint64_t seq = 0) {
+  uint32_t* cursors = reinterpret_cast<uint32_t*>(static_cast<char*>(slot->ptr) + kCursorOff);
+  if (!slot->cursors_clean) {
+    const hipError_t z = hipMemsetAsync(cursors, 0, 2 * kBucketCount * sizeof(uint32_t), stream);
+    if (z != hipSuccess) return hip_fail(z);
+    slot->cursors_clean = true;
+  }
+  const size_t rows_words = (size_t)bucket_grid(n) * kBucketCount;
   char* scratch = path_scratch(slot);
-  uint32_t* rows = reinterpret_cast<uint32_t*>(scratch);
-  uint32_t* ranges = rows + rows_words;
-  void* desc = scratch + head;
-  hipError_t e = launch_bucket(d_base, n, d_off, d_len, rows, ranges, desc, update ? nullptr : d_out, stream);
-  if (e != hipSuccess) rc = hip_fail(e);
+  BucketArgs bk{};
+  bk.base = d_base;
+  bk.rows = reinterpret_cast<uint32_t*>(scratch);
+  bk.ranges = bk.rows + rows_words;
+  bk.desc = scratch + (rows_words + 8) * sizeof(uint32_t);
+  const uint32_t set = (uint32_t)(slot->sorts & 1);
+  bk.cursor = cursors + set * kBucketCount;
+  bk.cursor_next = cursors + (set ^ 1) * kBucketCount;
+  bk.out = update ? nullptr : d_out;
+  uint32_t parts = 0;
+  hipError_t e = launch_extent(d_off, d_len, n, slot->ptr, &parts, &bk, stream);
+  if (e == hipSuccess) e = launch_bucket_place(d_off, d_len, n, slot->ptr, parts, bk, record, seq, stream);
+  if (e != hipSuccess) {
+    slot->cursors_clean = false;  // the next sort zeroes both sets first
+    return hip_fail(e);
+  }
+  slot->sorts++;
+  int rc = ANNETY_CRC_OK;
   const uint32_t groups[3] = {32, 16, 4};  // lanes per payload of the long / middle / small class
   for (int k = 0; k < 3 && rc == ANNETY_CRC_OK; k++)
-    rc = run_var(c, d_base, n, 0, 0, groups[k], desc, ranges + 2 * k, d_out, stream, update);
+    rc = run_var(c, d_base, n, 0, 0, groups[k], bk.desc, bk.ranges + 2 * k, d_out, stream, update);
   return rc;
 }
 
@@ -694,7 +719,7 @@ int run_arena(DeviceCtx& c, const void* d_base, size_t arena_bytes, const uint64
 // ---- automatic choice between the arena and the sorted path (annety_crc32_batch_var) ----
 // The arena path needs its extent on the host (grid, scratch) but the offsets are device data; reading them
 // back would make every call synchronous. Instead every call launches the extent kernel (crc32_kernels.h
-// launch_extent, ~2-3 us), which leaves the batch's extent in a pinned record per stream slot, and a call
+// launch_extent, ~5 us), which leaves the batch's extent in a pinned record per stream slot, and a call
 // takes the arena path over [lo, hi) when the two latest completed records for the same (base, offsets,
 // lengths, n) agree, are safe (sorted starts, gaps < 4 KiB) and dense (payload bytes >= 2/3 of the span).
 // The kernels then check this call's own extent against [lo, hi) on the device and, if it differs, read
@@ -766,23 +791,24 @@ int run_var_auto(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_o
     a.check_hi = h.hi;
     if (a.nsb && (rc = scratch_slot(c, stream, arena_geom(a).words * sizeof(uint32_t), &slot))) return rc;
   }
-  // this call's extent: the check the arena launches make, and the next calls' record
+  // this call's extent: the check the arena launches make, and the next calls' record (on the sorted
+  // path the bucket count runs in the same launch, and the bucket place publishes the record)
   const uint64_t seq = ++slot->calls;
-  uint32_t parts = 0;
-  hipError_t e = launch_extent(d_off, d_len, n, slot->ptr, grid_cus(c), &parts, stream);
-  if (e != hipSuccess) return hip_fail(e);
   (arena ? c.auto_arena : c.auto_sorted)++;
   if (arena) {
-    a.check = static_cast<const uint64_t*>(slot->ptr);
-    a.check_parts = parts;
-    a.record = slot->hint;
-    a.record_seq = seq;
-    a.scratch = reinterpret_cast<uint32_t*>(path_scratch(slot));
-    e = launch_arena(a, stream);
+    uint32_t parts = 0;
+    hipError_t e = launch_extent(d_off, d_len, n, slot->ptr, &parts, nullptr, stream);
+    if (e == hipSuccess) {
+      a.check = static_cast<const uint64_t*>(slot->ptr);
+      a.check_parts = parts;
+      a.record = slot->hint;
+      a.record_seq = seq;
+      a.scratch = reinterpret_cast<uint32_t*>(path_scratch(slot));
+      e = launch_arena(a, stream);
+    }
     rc = e == hipSuccess ? ANNETY_CRC_OK : hip_fail(e);
   } else {
-    e = launch_extent_publish(slot->ptr, parts, slot->hint, seq, stream);
-    rc = e == hipSuccess ? run_var_sorted_in(c, slot, d_base, n, d_off, d_len, d_out, stream, update) : hip_fail(e);
+    rc = run_var_sorted_in(c, slot, d_base, n, d_off, d_len, d_out, stream, update, slot->hint, seq);
   }
   const int rd = scratch_done(slot, stream);
   return rc ? rc : rd;

@@ -35,7 +35,7 @@ struct VarLaunch {
   size_t n;                  // payload count
   uint64_t fixed_stride;     // direct mode (desc == null): payload i at base + i*fixed_stride,
   uint32_t fixed_len;        //   fixed_len bytes
-  const void* desc;          // sorted mode: uint4 {addr lo, addr hi, len, index} per task (launch_bucket)
+  const void* desc;          // sorted mode: uint4 {addr lo, addr hi, len, index} per task (launch_bucket_place)
   const uint32_t* range;     // sorted mode: device [begin, end) into desc for this class
   uint32_t group;            // lanes per payload
   const void* img_slice;
@@ -48,15 +48,6 @@ struct VarLaunch {
 };
 
 hipError_t launch_var(const VarLaunch& a, hipStream_t stream);
-
-// Counting sort of a variable batch by 128-byte line count (longest first): writes desc[] (16 B per
-// non-empty payload), ranges[6] = {begin,end} of the G=32 / G=8 / G=2 classes, and out[p] = 0 for
-// zero-length payloads (out may be null: update mode leaves their registers alone). Scratch: rows = bucket_blocks(n) * bucket_count() words, ranges = 8 words,
-// desc = 16*n bytes.
-hipError_t launch_bucket(const void* base, size_t n, const uint64_t* d_off, const uint32_t* d_len, uint32_t* rows,
-                         uint32_t* ranges, void* desc, uint32_t* out, hipStream_t stream);
-unsigned bucket_blocks(size_t n);
-int bucket_count();
 
 // Long payloads cut into end-aligned segments (crc32_kernels.hip): descriptors for the variable kernel,
 // then the combine fold with powers[(m-1)*32 + bit] = shift_{m*seg}(1 << bit), m = 1..S-1.
@@ -73,6 +64,7 @@ hipError_t launch_split_join(const uint32_t* seg_crc, size_t n, uint32_t S, cons
 // (ExtentHint), whose `chk` = lo ^ hi ^ sum ^ bad ^ seq ^ kExtentCheck lets the host reject a record it read
 // while the device was rewriting it.
 constexpr size_t kExtentScratchBytes = 16384;
+constexpr uint32_t kExtentMaxParts = 128;  // partials (uint64 {lo, hi, sum, bad} at word 8 + 4b)
 constexpr uint64_t kExtentCheck = 0x9E3779B97F4A7C15ull;
 struct ExtentHint {
   uint64_t lo, hi, sum, bad;
@@ -111,11 +103,39 @@ struct ArenaLaunch {
   uint64_t record_seq;
 };
 
-// The per-block partials (returns their count in *parts); the arena launches reduce them themselves.
-hipError_t launch_extent(const uint64_t* off, const uint32_t* len, size_t n, void* ws, size_t max_blocks,
-                         uint32_t* parts, hipStream_t stream);
-// One block reducing the partials and publishing them to `host` (the sorted path, which has no stitch).
-hipError_t launch_extent_publish(const void* ws, uint32_t parts, ExtentHint* host, uint64_t seq, hipStream_t stream);
+// Counting sort of a variable batch by 128-byte line count, longest first, for the sorted path: two
+// launches, no host round trip and no memset per call.
+//  1. launch_extent with `bk`: besides the extent partials, each block histograms its payloads by line count
+//     in LDS and claims its slots in every bucket it uses with one agent-scope atomic add on that bucket's
+//     cursor (rows[b][i] = the value returned = block b's first slot inside bucket i, in arrival order),
+//     and writes out[p] = 0 for zero-length payloads (out null in update mode: their registers stay).
+//  2. launch_bucket_place: every block scans the 1024 cursor totals into bucket bases, ranks its payloads
+//     inside its slots with LDS atomics and writes desc[] (16 B per non-empty payload); block 0 writes the
+//     class ranges and zeroes the other cursor set for the next call (the two sets alternate per call, so
+//     the cursors are zero when a call's first launch starts), and, with `record`, publishes the extent.
+// The order of payloads inside a bucket depends on arrival order; the digests do not.
+constexpr uint32_t kBucketCount = 1024;
+constexpr uint32_t kBucketThreads = 1024;  // both launches; one payload per thread per grid stride
+constexpr size_t kCursorOff = 8192;        // the two cursor sets, in the extent scratch (2 x 4 KiB)
+static_assert((8 + 4 * kExtentMaxParts) * 8 <= kCursorOff && kCursorOff + 2 * 4 * kBucketCount <= kExtentScratchBytes,
+              "extent scratch layout");
+struct BucketArgs {
+  const void* base;       // payload offsets are relative to this pointer
+  uint32_t* rows;         // bucket_grid(n) * kBucketCount words
+  uint32_t* cursor;       // this call's set (zero on entry)
+  uint32_t* cursor_next;  // the other set: zeroed by launch_bucket_place
+  uint32_t* ranges;       // 6 words: {begin, end} of the G = 32 / 16 / 4 classes in desc
+  void* desc;             // uint4 {addr lo, addr hi, len, index} per non-empty payload
+  uint32_t* out;          // zero-length digests; null in update mode
+};
+unsigned bucket_grid(size_t n);  // blocks of both launches (= the extent partials: at most kExtentMaxParts)
+
+// The per-block extent partials (their count in *parts), and with `bk` step 1 of the counting sort.
+hipError_t launch_extent(const uint64_t* off, const uint32_t* len, size_t n, void* ws, uint32_t* parts,
+                         const BucketArgs* bk, hipStream_t stream);
+// Step 2 of the counting sort; `record` (nullable) receives the extent reduced from ws's partials.
+hipError_t launch_bucket_place(const uint64_t* off, const uint32_t* len, size_t n, const void* ws, uint32_t parts,
+                               const BucketArgs& bk, ExtentHint* record, uint64_t seq, hipStream_t stream);
 
 // Line-pass layout. L line-pass workgroups of 512 lanes = W = 8L waves = 64L lane groups;
 // wave w's task t is full superblock fs0 + t*W + w (lane group g = 8w + block). Per line of a full

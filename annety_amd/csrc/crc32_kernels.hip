@@ -216,7 +216,7 @@ __global__ __launch_bounds__(BLK) void crc32_oneround_kernel(const uint8_t* __re
 // Lines are assigned end-aligned over rounds of G lanes, exactly like the fixed kernel, and the
 // (task, round) steps are double-buffered across task boundaries.
 // `order`/`range` (optional) select the tasks: order[range[0] .. range[1]) are payload indices sorted
-// by line count (crc32_bucket_* below), so the payloads of a wave finish together and each length
+// by line count (crc32_bucket_place, crc32_arena.hip), so the payloads of a wave finish together and each length
 // class runs with its own G. Zero-length payloads never reach this kernel (the bucket pass writes 0).
 struct VarTask {
   uint64_t line0;    // absolute index of the payload's first 128-byte line
@@ -428,105 +428,6 @@ __global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __rest
   }
 }
 
-// ---- length bucketing for variable batches (counting sort by line count, longest first) ----
-// Three passes, no global atomics and no memset: per-block bucket histograms (rows), one scan that
-// turns them into per-(block, bucket) output bases, and a scatter that ranks payloads inside a
-// block with LDS atomics.
-constexpr int kBuckets = 1024;
-constexpr int kBucketBlock = 256;
-
-__device__ __forceinline__ uint32_t bucket_of(uint64_t a, uint32_t len) {
-  const uint32_t nl = (uint32_t)(((a + len - 1) >> 7) - (a >> 7) + 1);
-  return (uint32_t)(kBuckets - 1) - (nl < (uint32_t)(kBuckets - 1) ? nl : (uint32_t)(kBuckets - 1));
-}
-
-// Each block owns a contiguous tile of payloads (same tiling in hist and scatter).
-__device__ __forceinline__ void tile_of(size_t n, size_t& lo, size_t& hi) {
-  const size_t per = (n + gridDim.x - 1) / gridDim.x;
-  lo = (size_t)blockIdx.x * per;
-  lo = lo < n ? lo : n;
-  hi = lo + per < n ? lo + per : n;
-}
-
-__global__ __launch_bounds__(kBucketBlock) void crc32_bucket_hist(const uint8_t* __restrict__ base, size_t n,
-                                                                  const uint64_t* __restrict__ d_off,
-                                                                  const uint32_t* __restrict__ d_len,
-                                                                  uint32_t* __restrict__ rows,
-                                                                  uint32_t* __restrict__ out) {
-  __shared__ uint32_t h[kBuckets];
-  for (int i = threadIdx.x; i < kBuckets; i += kBucketBlock) h[i] = 0;
-  __syncthreads();
-  size_t lo, hi;
-  tile_of(n, lo, hi);
-  for (size_t p = lo + threadIdx.x; p < hi; p += kBucketBlock) {
-    const uint32_t len = d_len[p];
-    if (len == 0) {
-      if (out) out[p] = 0u;  // crc of the empty string (update mode: the register is unchanged)
-      continue;
-    }
-    atomicAdd(&h[bucket_of((uint64_t)(uintptr_t)(base + d_off[p]), len)], 1u);
-  }
-  __syncthreads();
-  uint32_t* row = rows + (size_t)blockIdx.x * kBuckets;
-  for (int i = threadIdx.x; i < kBuckets; i += kBucketBlock) row[i] = h[i];
-}
-
-// rows[b][i] (counts) -> rows[b][i] = output base of block b's payloads in bucket i, buckets in
-// order, blocks in order inside a bucket; ranges = {begin,end} of the G=32 / G=8 / G=2 classes.
-__global__ __launch_bounds__(kBuckets) void crc32_bucket_scan(uint32_t* __restrict__ rows, uint32_t nblocks,
-                                                              uint32_t* __restrict__ ranges) {
-  __shared__ uint32_t sc[kBuckets];
-  const int i = threadIdx.x;
-  uint32_t tot = 0;
-  for (uint32_t b = 0; b < nblocks; b++) tot += rows[(size_t)b * kBuckets + i];
-  sc[i] = tot;
-  __syncthreads();
-  for (int d = 1; d < kBuckets; d <<= 1) {
-    const uint32_t v = i >= d ? sc[i - d] : 0u;
-    __syncthreads();
-    sc[i] += v;
-    __syncthreads();
-  }
-  uint32_t run = sc[i] - tot;  // exclusive start of bucket i
-  for (uint32_t b = 0; b < nblocks; b++) {
-    const uint32_t c = rows[(size_t)b * kBuckets + i];
-    rows[(size_t)b * kBuckets + i] = run;
-    run += c;
-  }
-  // classes by line count (bucket = 1023 - lines): >= 128 lines, 24..127, < 24, run at G = 32 / 16 / 4
-  // (crc32_capi.cpp run_var_sorted; on the config-3 batch the middle and small classes ran 12 % and
-  // 15 % faster at G = 16 / 4 than at 8 / 2: profiles/r02/ab4_stages.log).
-  constexpr int b8 = kBuckets - 128, b2 = kBuckets - 24;  // first bucket of the middle / small classes
-  if (i == 0) {
-    ranges[0] = 0;
-    ranges[1] = sc[b8 - 1];        // long class: buckets [0, b8)
-    ranges[2] = sc[b8 - 1];
-    ranges[3] = sc[b2 - 1];        // middle class: buckets [b8, b2)
-    ranges[4] = sc[b2 - 1];
-    ranges[5] = sc[kBuckets - 1];  // small class: buckets [b2, kBuckets)
-  }
-}
-
-__global__ __launch_bounds__(kBucketBlock) void crc32_bucket_scatter(const uint8_t* __restrict__ base, size_t n,
-                                                                     const uint64_t* __restrict__ d_off,
-                                                                     const uint32_t* __restrict__ d_len,
-                                                                     const uint32_t* __restrict__ rows,
-                                                                     uint4* __restrict__ desc) {
-  __shared__ uint32_t basep[kBuckets];
-  const uint32_t* row = rows + (size_t)blockIdx.x * kBuckets;
-  for (int i = threadIdx.x; i < kBuckets; i += kBucketBlock) basep[i] = row[i];
-  __syncthreads();
-  size_t lo, hi;
-  tile_of(n, lo, hi);
-  for (size_t p = lo + threadIdx.x; p < hi; p += kBucketBlock) {
-    const uint32_t len = d_len[p];
-    if (!len) continue;
-    const uint64_t a = (uint64_t)(uintptr_t)(base + d_off[p]);
-    const uint32_t pos = atomicAdd(&basep[bucket_of(a, len)], 1u);  // LDS atomic: rank inside the block
-    desc[pos] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), len, (uint32_t)p);
-  }
-}
-
 // ---- long payloads: segments + CRC combine ----
 // A batch of few long payloads cannot fill 256 CUs with at most 32 lanes per payload, and a batch
 // whose payload count is not a multiple of the lane-groups leaves a tail. Such payloads are cut into
@@ -684,17 +585,6 @@ hipError_t launch_var(const VarLaunch& a, hipStream_t stream) {
   }
 }
 
-hipError_t launch_bucket(const void* base, size_t n, const uint64_t* d_off, const uint32_t* d_len,
-                         uint32_t* rows, uint32_t* ranges, void* desc, uint32_t* out, hipStream_t stream) {
-  const unsigned blocks = bucket_blocks(n);
-  hipLaunchKernelGGL(crc32_bucket_hist, dim3(blocks), dim3(kBucketBlock), 0, stream,
-                     static_cast<const uint8_t*>(base), n, d_off, d_len, rows, out);
-  hipLaunchKernelGGL(crc32_bucket_scan, dim3(1), dim3(kBuckets), 0, stream, rows, blocks, ranges);
-  hipLaunchKernelGGL(crc32_bucket_scatter, dim3(blocks), dim3(kBucketBlock), 0, stream,
-                     static_cast<const uint8_t*>(base), n, d_off, d_len, rows, static_cast<uint4*>(desc));
-  return hipGetLastError();
-}
-
 hipError_t launch_split_desc(const void* base, size_t n, uint64_t len, uint64_t stride, uint64_t seg, uint32_t S,
                              void* desc, uint32_t* range, hipStream_t stream) {
   const size_t total = n * (size_t)S;
@@ -715,13 +605,6 @@ hipError_t launch_split_join(const uint32_t* seg_crc, size_t n, uint32_t S, cons
   hipLaunchKernelGGL(crc32_split_join, dim3(blocks), dim3(256), 0, stream, seg_crc, n, S, powers, out);
   return hipGetLastError();
 }
-
-unsigned bucket_blocks(size_t n) {
-  // ~4K payloads per block keeps the scan's per-bucket walk short; at most 256 rows
-  return (unsigned)std::max<size_t>(1, std::min<size_t>(256, (n + 4095) / 4096));
-}
-
-int bucket_count() { return kBuckets; }
 
 int fixed_kernel_block() { return kBlock; }
 

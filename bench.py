@@ -223,8 +223,8 @@ class Workload:
                            "(annety_amd/csrc/crc32_arena.hip, crc32_arena_lines.h)" if self.arena else
                            "crc32_extent_kernel + (arena or sorted path, chosen per call), one step "
                            "(annety_amd/csrc/crc32_capi.cpp run_var_auto)" if args.var_path == "auto" else
-                           "crc32_bucket_hist/scan/scatter + crc32_var_kernel<32/8/2>, one step "
-                           "(annety_amd/csrc/crc32_kernels.hip)")
+                           "crc32_extent_kernel<count> + crc32_bucket_place + crc32_var_kernel<32/16/4>, one step "
+                           "(annety_amd/csrc/crc32_arena.hip, crc32_kernels.hip)")
             self.desc = (f"BASELINE config 3: {self.n} payloads, Zipf(1.1) lengths 64 B-64 KiB packed unaligned, "
                          f"{total / 2**30:.3f} GiB per GPU, " + {"arena": "arena path", "auto": "automatic path choice",
                                                                   "sorted": "sorted path"}[args.var_path])

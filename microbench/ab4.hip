@@ -70,9 +70,11 @@ int main() {
   STAGE("warm fixed batches");
   RC(annety_crc32_batch_var(d, doff, dlen, n, ref, nullptr));
   STAGE("reference batch_var");
-  const size_t rows_words = (size_t)bucket_blocks(n) * bucket_count();
-  uint32_t *rows, *ranges; void* desc;
+  const size_t rows_words = (size_t)bucket_grid(n) * kBucketCount;
+  uint32_t *rows, *ranges; void *desc, *ws;
   CK(hipMalloc(&rows, rows_words * 4)); CK(hipMalloc(&ranges, 64)); CK(hipMalloc(&desc, 16 * n));
+  CK(hipMalloc(&ws, kExtentScratchBytes)); CK(hipMemset(ws, 0, kExtentScratchBytes));
+  uint64_t sorts = 0;
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   auto b2b = [&](auto launch, const char* name, bool check) {
     for (int w = 0; w < 5; w++) launch();
@@ -90,7 +92,14 @@ int main() {
     }
     printf("%-40s %.4f ms  %.1f GB/s %s\n", name, ms / 30, total / (ms / 30) / 1e6, check ? (ok ? "ok" : "MISMATCH") : "");
   };
-  auto bucket = [&] { CK(launch_bucket(d, n, doff, dlen, rows, ranges, desc, out, nullptr)); };
+  auto bucket = [&] {  // the product's two-launch counting sort (crc32_kernels.h BucketArgs)
+    uint32_t* cur = reinterpret_cast<uint32_t*>(static_cast<char*>(ws) + kCursorOff);
+    const uint32_t set = (uint32_t)(sorts++ & 1);
+    BucketArgs bk{d, rows, cur + set * kBucketCount, cur + (set ^ 1) * kBucketCount, ranges, desc, out};
+    uint32_t parts = 0;
+    CK(launch_extent(doff, dlen, n, ws, &parts, &bk, nullptr));
+    CK(launch_bucket_place(doff, dlen, n, ws, parts, bk, nullptr, 0, nullptr));
+  };
   b2b([&] { RC(annety_crc32_batch_var(d, doff, dlen, n, out, nullptr)); }, "product batch_var", true);
   b2b(bucket, "bucket passes only", false);
   bucket();
