@@ -28,6 +28,7 @@ from .crc32c import (  # noqa: F401
     reserve_cus,
     scratch_stats,
     set_split,
+    set_walk_segment,
     stream_release,
     var_path_stats,
     tables,
@@ -49,6 +50,7 @@ __all__ = [
     "reserve_cus",
     "scratch_stats",
     "set_split",
+    "set_walk_segment",
     "stream_release",
     "var_path_stats",
     "tables",

@@ -23,6 +23,7 @@ SIGNATURES = [
     ("annety_crc_last_hip_error", ctypes.c_int, []),
     ("annety_crc_reserve_cus", ctypes.c_int, [ctypes.c_int]),
     ("annety_crc_set_split", ctypes.c_int, [ctypes.c_int, _u64]),
+    ("annety_crc_set_walk_segment", ctypes.c_int, [_u64]),
     ("annety_crc_stream_release", ctypes.c_int, [_vp]),
     ("annety_crc_var_path_stats", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
     ("annety_crc_scratch_stats", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_u64), ctypes.POINTER(_u64),

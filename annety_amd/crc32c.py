@@ -81,6 +81,11 @@ def reserve_cus(n: int) -> None:
     _lib.check(_lib.get().annety_crc_reserve_cus(int(n)), "annety_crc_reserve_cus")
 
 
+def set_walk_segment(nbytes: int = 0) -> None:
+    """annety_crc_set_walk_segment: segment size of the host frame walks (0 = default 64 MiB), process-wide."""
+    _lib.check(_lib.get().annety_crc_set_walk_segment(int(nbytes)), "annety_crc_set_walk_segment")
+
+
 def set_split(mode: int = -1, min_segment: int = 0) -> None:
     """annety_crc_set_split: long-payload split policy (-1 auto, 0 never, 1 always), process-wide."""
     _lib.check(_lib.get().annety_crc_set_split(int(mode), int(min_segment)), "annety_crc_set_split")

@@ -1284,41 +1284,216 @@ static FrameRules lhc_rules(int T, int64_t max_payload) { return {T, 4, max_payl
 // > 64 MiB (:229-233).
 static constexpr FrameRules kPbcRules = {4, 10, 64ll << 20, 6, 64ll << 20};
 
+// ---- frame walks: LengthHeaderCodec::decode's framing (include/codec/LengthHeaderCodec.h:71-137) over a
+// host buffer, a dependent chain of one header read per frame (~140-170 ns a frame from DRAM) ----
+// A buffer of at least two walk segments (annety_crc_set_walk_segment, default 64 MiB) is walked in
+// segments side by side. Segment 0 is walked from offset 0 as the codec does. Every later segment first
+// looks for a speculative entry: the first position in its first kSpecProbe bytes from which kSpecHops
+// frames in a row parse. It walks from there to its end. The walks are then joined in order: the true walk
+// (from offset 0) continues frame by frame until it lands on a header the next segment's walk recorded;
+// from that header on, both walks are the same chain, so that segment's frames are taken as they are. A
+// segment whose entry was wrong (payload bytes that parse as headers) is walked again by the join, frame by
+// frame: speculation costs time, never a different result.
+namespace {
+enum class Step { kFrame, kInvalid, kIncomplete, kTooBig };
+
+// The frame whose header starts at `pos`; *length = its length field (payload + 4 checksum bytes).
+inline Step frame_at(const FrameRules& r, const unsigned char* p, size_t size, size_t pos, int64_t* length) {
+  const size_t T = (size_t)r.T;
+  if (pos > size || size - pos < T) return Step::kIncomplete;
+  uint64_t u = 0;
+  for (size_t b = 0; b < T; b++) u = (u << 8) | p[pos + b];
+  switch (T) {  // sign-extend like peek_int8/16/32/64
+    case 1: *length = (int8_t)u; break;
+    case 2: *length = (int16_t)u; break;
+    case 4: *length = (int32_t)u; break;
+    default: *length = (int64_t)u; break;
+  }
+  if (*length < r.dec_min || (r.dec_max > 0 && *length > r.dec_max)) return Step::kInvalid;  // decode: -1
+  if (size - pos - T < (uint64_t)*length) return Step::kIncomplete;                           // decode: 0
+  if (*length - 4 > 0xFFFFFFFFll) return Step::kTooBig;  // valid for the codec, beyond 32-bit lengths
+  return Step::kFrame;
+}
+inline int step_rt(Step s) { return s == Step::kInvalid ? 1 : s == Step::kTooBig ? ANNETY_CRC_EINVAL : 0; }
+
+struct ConnWalk {
+  std::vector<uint64_t> off;  // payload offsets, relative to the buffer
+  std::vector<uint32_t> len;
+  size_t consumed = 0;        // where the walk stopped
+  int rt = 0;                 // 0, 1 (invalid length) or ANNETY_CRC_EINVAL (a frame beyond 32-bit lengths)
+  bool ended = false;         // stopped by the stream itself, not by its stop position or the frame cap
+};
+
+// Frames from header position `pos` while pos < stop_at, at most `cap` of them in w.
+void walk_range(const FrameRules& r, const unsigned char* p, size_t size, size_t pos, size_t stop_at, size_t cap,
+                ConnWalk& w) {
+  const size_t T = (size_t)r.T;
+  while (pos < stop_at && w.off.size() < cap) {
+    int64_t L = 0;
+    const Step st = frame_at(r, p, size, pos, &L);
+    if (st != Step::kFrame) {
+      w.ended = true;
+      w.rt = step_rt(st);
+      break;
+    }
+    w.off.push_back(pos + T);
+    w.len.push_back((uint32_t)(L - 4));
+    pos += T + (size_t)L;
+  }
+  w.consumed = pos;
+}
+
+std::atomic<uint64_t> g_walk_seg{64ull << 20};
+constexpr size_t kWalkMaxSegs = 64;
+constexpr size_t kSpecProbe = 1u << 20;
+
+// Segment [lo, hi) of a buffer (not the first): a speculative entry, then the walk from it up to hi.
+void walk_segment(const FrameRules& r, const unsigned char* p, size_t size, size_t lo, size_t hi, size_t cap,
+                  ConnWalk& w) {
+  const size_t T = (size_t)r.T;
+  const int hops = T == 1 ? 32 : T == 2 ? 16 : 8;  // short length fields parse by chance more often
+  const size_t end = std::min(size, lo + kSpecProbe);
+  for (size_t q = lo; q < end; q++) {
+    size_t pos = q;
+    int h = 0;
+    int64_t L = 0;
+    for (; h < hops && frame_at(r, p, size, pos, &L) == Step::kFrame; h++) pos += T + (size_t)L;
+    if (h == hops) {
+      walk_range(r, p, size, q, hi, cap, w);
+      return;
+    }
+  }
+  w.consumed = SIZE_MAX;  // no entry found: the join walks this segment itself
+}
+
+// The walks of k buffers, on walker threads; join() leaves walks()[c] = buffer c's walk from offset 0.
+class FrameWalks {
+ public:
+  FrameWalks(const FrameRules& r, const void* const* bufs, const size_t* sizes, size_t k, size_t cap)
+      : r_(r), bufs_(bufs), sizes_(sizes), cap_(cap), bounds_(k), segs_(k), walks_(k) {
+    const size_t seg = (size_t)g_walk_seg.load();
+    for (size_t c = 0; c < k; c++) {
+      const size_t m = std::max<size_t>(1, std::min<size_t>(kWalkMaxSegs, sizes[c] / seg));
+      bounds_[c].resize(m + 1);
+      for (size_t i = 0; i < m; i++) bounds_[c][i] = sizes[c] / m * i;
+      bounds_[c][m] = SIZE_MAX;  // the last segment walks to the stream's end
+      segs_[c].resize(m);
+      for (size_t i = 0; i < m; i++) tasks_.push_back({c, i});
+    }
+  }
+  ~FrameWalks() { join_threads(); }
+  void start(size_t max_threads) {
+    const size_t n = std::min(tasks_.size(), std::max<size_t>(1, max_threads));
+    for (size_t t = 0; t < n; t++)
+      threads_.emplace_back([this] {
+        for (size_t i; (i = next_.fetch_add(1)) < tasks_.size();) run(tasks_[i]);
+      });
+  }
+  void join() {  // idempotent
+    join_threads();
+    if (joined_) return;
+    joined_ = true;
+    for (size_t c = 0; c < walks_.size(); c++) splice(c);
+  }
+  std::vector<ConnWalk>& walks() { return walks_; }
+
+ private:
+  struct Task {
+    size_t c, i;
+  };
+  const unsigned char* buf(size_t c) const { return static_cast<const unsigned char*>(bufs_[c]); }
+  void run(const Task& t) {
+    const size_t lo = bounds_[t.c][t.i], hi = bounds_[t.c][t.i + 1];
+    if (t.i == 0)
+      walk_range(r_, buf(t.c), sizes_[t.c], 0, hi, cap_, segs_[t.c][0]);
+    else
+      walk_segment(r_, buf(t.c), sizes_[t.c], lo, hi, cap_, segs_[t.c][t.i]);
+  }
+  void join_threads() {
+    for (auto& th : threads_)
+      if (th.joinable()) th.join();
+    threads_.clear();
+  }
+  void splice(size_t c) {
+    std::vector<ConnWalk>& segs = segs_[c];
+    ConnWalk& out = walks_[c];
+    out = std::move(segs[0]);
+    const unsigned char* p = buf(c);
+    const size_t size = sizes_[c], T = (size_t)r_.T;
+    size_t pos = out.consumed;
+    for (size_t i = 1; i < segs.size() && !out.ended && out.off.size() < cap_; i++) {
+      ConnWalk& s = segs[i];
+      const size_t hi = bounds_[c][i + 1];
+
+      while (!out.ended && out.off.size() < cap_ && pos < hi) {
+        const auto it = std::lower_bound(s.off.begin(), s.off.end(), (uint64_t)pos + T);
+        if (it != s.off.end() && *it == pos + T) {  // the true walk reached a header of the segment's walk
+          const size_t j = (size_t)(it - s.off.begin());
+          const size_t take = std::min(s.off.size() - j, cap_ - out.off.size());
+          out.off.insert(out.off.end(), s.off.begin() + j, s.off.begin() + j + take);
+          out.len.insert(out.len.end(), s.len.begin() + j, s.len.begin() + j + take);
+          if (j + take < s.off.size()) {  // cut by the frame cap
+            pos = out.off.back() + out.len.back() + 4;
+            break;
+          }
+          pos = s.consumed;  // the segment's end, its own cap (go on frame by frame) or the stream's end
+          if (s.ended) {
+            out.ended = true;
+            out.rt = s.rt;
+          }
+          continue;
+        }
+        int64_t L = 0;
+        const Step st = frame_at(r_, p, size, pos, &L);
+        if (st != Step::kFrame) {
+          out.ended = true;
+          out.rt = step_rt(st);
+          break;
+        }
+        out.off.push_back(pos + T);
+        out.len.push_back((uint32_t)(L - 4));
+        pos += T + (size_t)L;
+      }
+    }
+    out.consumed = pos;
+    segs.clear();
+  }
+
+  const FrameRules r_;
+  const void* const* bufs_;
+  const size_t* sizes_;
+  const size_t cap_;
+  std::vector<std::vector<size_t>> bounds_;
+  std::vector<std::vector<ConnWalk>> segs_;
+  std::vector<ConnWalk> walks_;
+  std::vector<Task> tasks_;
+  std::atomic<size_t> next_{0};
+  std::vector<std::thread> threads_;
+  bool joined_ = false;
+};
+
+size_t walker_threads() { return std::max(1u, std::min(8u, std::thread::hardware_concurrency())); }
+}  // namespace
+
 static int parse_frames(const FrameRules& r, const void* h_stream, size_t size, uint64_t* payload_off,
                         uint32_t* payload_len, size_t max_frames, size_t* n_frames, size_t* consumed) {
   if (!n_frames || !consumed || !lhc_type_ok(r.T) || (!h_stream && size) || (max_frames && (!payload_off || !payload_len)))
     return ANNETY_CRC_EINVAL;
-  const unsigned char* p = static_cast<const unsigned char*>(h_stream);
-  const size_t T = (size_t)r.T;
-  size_t pos = 0, k = 0;
-  int rc = ANNETY_CRC_OK;
-  while (k < max_frames && size - pos >= T) {
-    uint64_t u = 0;
-    for (size_t b = 0; b < T; b++) u = (u << 8) | p[pos + b];
-    int64_t length;  // sign-extend like peek_int8/16/32/64
-    switch (T) {
-      case 1: length = (int8_t)u; break;
-      case 2: length = (int16_t)u; break;
-      case 4: length = (int32_t)u; break;
-      default: length = (int64_t)u; break;
-    }
-    if (length < r.dec_min || (r.dec_max > 0 && length > r.dec_max)) {
-      rc = 1;  // decode returns -1: invalid length
-      break;
-    }
-    if (size - pos - T < (uint64_t)length) break;  // incomplete frame (decode returns 0)
-    if (length - 4 > 0xFFFFFFFFll) {  // a complete frame valid for the codec, beyond this API's 32-bit lengths
-      rc = ANNETY_CRC_EINVAL;
-      break;
-    }
-    payload_off[k] = pos + T;
-    payload_len[k] = (uint32_t)(length - 4);
-    k++;
-    pos += T + (size_t)length;
-  }
-  *n_frames = k;
-  *consumed = pos;
-  return rc;
+  FrameWalks fw(r, &h_stream, &size, 1, max_frames);
+  fw.start(walker_threads());
+  fw.join();
+  const ConnWalk& w = fw.walks()[0];
+  std::copy(w.off.begin(), w.off.end(), payload_off);
+  std::copy(w.len.begin(), w.len.end(), payload_len);
+  *n_frames = w.off.size();
+  *consumed = w.consumed;
+  return w.rt;
+}
+
+int annety_crc_set_walk_segment(uint64_t bytes) {
+  if (bytes && bytes < 4096) return ANNETY_CRC_EINVAL;
+  g_walk_seg.store(bytes ? bytes : 64ull << 20);
+  return ANNETY_CRC_OK;
 }
 
 // include/codec/LengthHeaderCodec.h:71-137 without the CRC: signed big-endian length (peek_int*),
@@ -1433,45 +1608,6 @@ int annety_pbc_encode_batch(const void* d_src, const uint64_t* d_src_off, const 
 // header walk - a dependent chain of one header read per frame, ~140-170 ns a frame from DRAM - runs on
 // its own walker thread (connections are independent), while the buffers are packed into pinned memory
 // and uploaded (pinned buffers, e.g. annety_crc_host_register'ed NetBuffer arenas, are DMA'd in place).
-namespace {
-struct ConnWalk {
-  std::vector<uint64_t> off;  // relative to the connection's buffer
-  std::vector<uint32_t> len;
-  size_t consumed = 0;
-  int rt = 0;
-};
-
-// LengthHeaderCodec::decode's framing over one buffer, at most `cap` frames (parse_frames' rules).
-void walk_conn(const FrameRules& r, const unsigned char* p, size_t size, size_t cap, ConnWalk& w) {
-  const size_t T = (size_t)r.T;
-  size_t pos = 0;
-  while (w.off.size() < cap && size - pos >= T) {
-    uint64_t u = 0;
-    for (size_t b = 0; b < T; b++) u = (u << 8) | p[pos + b];
-    int64_t length;  // sign-extend like peek_int8/16/32/64
-    switch (T) {
-      case 1: length = (int8_t)u; break;
-      case 2: length = (int16_t)u; break;
-      case 4: length = (int32_t)u; break;
-      default: length = (int64_t)u; break;
-    }
-    if (length < r.dec_min || (r.dec_max > 0 && length > r.dec_max)) {
-      w.rt = 1;  // decode returns -1: invalid length
-      break;
-    }
-    if (size - pos - T < (uint64_t)length) break;  // incomplete frame (decode returns 0)
-    if (length - 4 > 0xFFFFFFFFll) {
-      w.rt = ANNETY_CRC_EINVAL;  // a complete frame valid for the codec, beyond this API's 32-bit lengths
-      break;
-    }
-    w.off.push_back(pos + T);
-    w.len.push_back((uint32_t)(length - 4));
-    pos += T + (size_t)length;
-  }
-  w.consumed = pos;
-}
-}  // namespace
-
 static int verify_host_iov(const FrameRules& r, const void* const* h_bufs, const size_t* sizes, size_t k,
                            uint64_t* h_payload_off, uint32_t* h_payload_len, uint8_t* h_ok, size_t max_frames,
                            size_t* conn_frames, size_t* conn_consumed, int* conn_rt) {
@@ -1487,20 +1623,11 @@ static int verify_host_iov(const FrameRules& r, const void* const* h_bufs, const
   }
   const uint64_t total = base[k];
   if (total == 0 || max_frames == 0) return ANNETY_CRC_OK;
-  // the walks: connections are independent, one walker thread per connection up to a pool's worth
-  std::vector<ConnWalk> walks(k);
-  std::atomic<size_t> next{0};
-  auto walker = [&] {
-    for (size_t c; (c = next.fetch_add(1)) < k;)
-      walk_conn(r, static_cast<const unsigned char*>(h_bufs[c]), sizes[c], max_frames, walks[c]);
-  };
-  const size_t nwalk = std::min<size_t>(k, std::max<size_t>(1, std::min(8u, std::thread::hardware_concurrency())));
-  std::vector<std::thread> walkers;
-  for (size_t i = 0; i < nwalk; i++) walkers.emplace_back(walker);
-  auto join_walkers = [&] {
-    for (auto& t : walkers)
-      if (t.joinable()) t.join();
-  };
+  // the walks (connections, and segments of large buffers, side by side: FrameWalks) run on their own
+  // threads while the bytes are packed and uploaded
+  FrameWalks fw(r, h_bufs, sizes, k, max_frames);
+  fw.start(walker_threads());
+  auto join_walkers = [&] { fw.join(); };
   DeviceCtx* c = nullptr;
   int rc = stream_ctx(nullptr, &c);
   if (rc) {
@@ -1557,6 +1684,7 @@ static int verify_host_iov(const FrameRules& r, const void* const* h_bufs, const
     }
   }
   join_walkers();
+  std::vector<ConnWalk>& walks = fw.walks();
   // frames in connection order, the output bound applied in that order (Codec::recv's per-connection
   // results; a connection cut by the bound stops as annety_lhc_parse does at max_frames: rt 0)
   size_t nf = 0;

@@ -65,6 +65,11 @@ int annety_crc_reserve_cus(int n);
  * payload spans two segments; min_segment = smallest segment in bytes (power of two >= 4096), 0 = default
  * 64 KiB. Digests do not depend on it. */
 int annety_crc_set_split(int mode, uint64_t min_segment);
+/* Host frame walks (annety_lhc_parse, annety_*_verify_host*): a buffer of at least two segments of
+ * `bytes` (0 = default 64 MiB, at least 4096) is walked in segments side by side, each later segment from
+ * a speculative entry that the in-order join confirms or redoes (crc32_capi.cpp FrameWalks). Results do
+ * not depend on it. Process-wide. */
+int annety_crc_set_walk_segment(uint64_t bytes);
 /* Drops `stream`'s per-stream scratch on the current device (stream-ordered free, no wait). Call before
  * destroying a stream that ran variable, arena or split batches. */
 int annety_crc_stream_release(void* stream);

@@ -115,3 +115,34 @@ def test_update_mode_auto(gpu):
         want = oracle.batch_var_mt(data, offs.astype(np.uint64), lens.astype(np.uint32), threads=8, states=want)
         torch.cuda.synchronize()
         assert np.array_equal(state.cpu().numpy().view(np.uint32), want)
+
+
+def test_sorted_calls_back_to_back(gpu):
+    """The sorted path's counting sort alternates two cursor sets per stream slot, each zeroed by the call
+    before (crc32_kernels.h BucketArgs): ten calls on one stream with no wait between them, alternating the
+    explicit sorted entry (n < 1024) and the automatic one (sparse, unsorted batches of 1024+ payloads with
+    empty payloads), each with its own batch and all checked afterwards."""
+    import torch
+
+    import annety_amd
+
+    cases, outs = [], []
+    for i in range(10):
+        n = 700 + 37 * i if i % 2 == 0 else 2500 + 301 * i
+        rng = np.random.default_rng(100 + i)
+        lens = np.minimum(40000, 64 * rng.zipf(1.4, n) + rng.integers(0, 300, n)).astype(np.int64)
+        lens[rng.integers(0, n, n // 20)] = 0
+        offs = np.concatenate([[0], np.cumsum(lens + 5000)[:-1]]).astype(np.int64)
+        perm = rng.permutation(n)  # unsorted descriptors
+        offs, lens = offs[perm].copy(), lens[perm].copy()
+        data = rng.integers(0, 256, int((offs + lens).max()) + 256, dtype=np.uint8)
+        cases.append((data, offs, lens, _dev(gpu, data, offs, lens)))
+    s0 = annety_amd.var_path_stats(0)
+    for data, offs, lens, (d, o, ln) in cases:
+        out = torch.full((len(lens),), 7, dtype=torch.int32, device=gpu)
+        annety_amd.crc32_batch_var(d, o, ln, out=out)
+        outs.append(out)
+    for (data, offs, lens, _), out in zip(cases, outs):
+        _check(out, data, offs, lens)
+    s1 = annety_amd.var_path_stats(0)
+    assert s1["arena"] == s0["arena"] and s1["sorted"] - s0["sorted"] == 5, (s0, s1)
