@@ -68,6 +68,17 @@ def recv_result(length_type: int, off: np.ndarray, ln: np.ndarray, used: int, in
     return DecodeResult(off, ln, used, -1 if invalid else 0, ok)
 
 
+def _frame_caps(worst: int, max_frames):
+    """Output bounds to try in turn. The result arrays are sized by the bound, and worst-case arrays (a
+    frame per T + 4 bytes) for a 1 GiB buffer cost more than the verify itself (1.7 GB of fresh arrays per
+    call: 20 against 49 GiB/s): first a bound for frames of 128 bytes or more on
+    average, the worst case only when a call filled that one (and is then repeated)."""
+    if max_frames is not None:
+        return [int(max_frames)]
+    first = min(worst, worst // 16 + 4096)
+    return [first] if first >= worst else [first, worst]
+
+
 def _iov_results(call, name, length_type, streams, max_frames):
     """Shared body of decode_host_iov: K receive buffers through one *_verify_host_iov call; returns one
     DecodeResult per buffer (what Codec::recv would have produced on that connection)."""
@@ -75,16 +86,19 @@ def _iov_results(call, name, length_type, streams, max_frames):
     k = len(views)
     addrs = (ctypes.c_void_p * max(k, 1))(*[v[0] or None for v in views])
     sizes = np.array([v[1] for v in views] or [0], dtype=np.uint64)
-    cap = sum(v[1] // (length_type + 4) + 1 for v in views) if max_frames is None else int(max_frames)
-    off = np.zeros(max(cap, 1), dtype=np.uint64)
-    ln = np.zeros(max(cap, 1), dtype=np.uint32)
-    ok = np.zeros(max(cap, 1), dtype=np.uint8)
-    nfr = np.zeros(max(k, 1), dtype=np.uint64)
-    used = np.zeros(max(k, 1), dtype=np.uint64)
-    rts = np.zeros(max(k, 1), dtype=np.int32)
-    st = call(addrs, sizes.ctypes.data, k, off.ctypes.data, ln.ctypes.data, ok.ctypes.data, cap, nfr.ctypes.data,
-              used.ctypes.data, rts.ctypes.data)
-    _lib.check(st, name)
+    caps = _frame_caps(sum(v[1] // (length_type + 4) + 1 for v in views), max_frames)
+    for cap in caps:
+        off = np.empty(max(cap, 1), dtype=np.uint64)
+        ln = np.empty(max(cap, 1), dtype=np.uint32)
+        ok = np.empty(max(cap, 1), dtype=np.uint8)
+        nfr = np.zeros(max(k, 1), dtype=np.uint64)
+        used = np.zeros(max(k, 1), dtype=np.uint64)
+        rts = np.zeros(max(k, 1), dtype=np.int32)
+        st = call(addrs, sizes.ctypes.data, k, off.ctypes.data, ln.ctypes.data, ok.ctypes.data, cap, nfr.ctypes.data,
+                  used.ctypes.data, rts.ctypes.data)
+        _lib.check(st, name)
+        if int(nfr[:k].sum()) < cap:
+            break
     out, pos = [], 0
     for c in range(k):
         n = int(nfr[c])
@@ -117,14 +131,16 @@ class LengthHeaderCodec:
         """Host header walk (annety_lhc_parse): (payload_off u64[k], payload_len u32[k], consumed,
         stopped_on_invalid_length)."""
         addr, size, keep = _host_view(stream)
-        cap = size // (self.length_type + 4) + 1 if max_frames is None else int(max_frames)
-        off = np.zeros(cap, dtype=np.uint64)
-        ln = np.zeros(cap, dtype=np.uint32)
-        k, used = ctypes.c_size_t(), ctypes.c_size_t()
-        st = _lib.get().annety_lhc_parse(addr or None, size, self.length_type, self.max_payload, off.ctypes.data,
-                                         ln.ctypes.data, cap, ctypes.byref(k), ctypes.byref(used))
-        if st < 0:
-            _lib.check(st, "annety_lhc_parse")
+        for cap in _frame_caps(size // (self.length_type + 4) + 1, max_frames):
+            off = np.empty(cap, dtype=np.uint64)
+            ln = np.empty(cap, dtype=np.uint32)
+            k, used = ctypes.c_size_t(), ctypes.c_size_t()
+            st = _lib.get().annety_lhc_parse(addr or None, size, self.length_type, self.max_payload, off.ctypes.data,
+                                             ln.ctypes.data, cap, ctypes.byref(k), ctypes.byref(used))
+            if st < 0:
+                _lib.check(st, "annety_lhc_parse")
+            if k.value < cap:
+                break
         return off[: k.value], ln[: k.value], int(used.value), st == 1
 
     def verify(self, d_stream, d_off, d_len, out_ok=None, out_digest=None, stream=None, arena=True):
@@ -174,15 +190,18 @@ class LengthHeaderCodec:
         """Codec::recv over a host receive buffer in one call (annety_lhc_verify_host): the header walk
         overlaps the stream's copy to the current device, the CRCs are checked there."""
         addr, size, keep = _host_view(stream)
-        cap = size // (self.length_type + 4) + 1 if max_frames is None else int(max_frames)
-        off = np.zeros(cap, dtype=np.uint64)
-        ln = np.zeros(cap, dtype=np.uint32)
-        ok = np.zeros(cap, dtype=np.uint8)
-        k, used = ctypes.c_size_t(), ctypes.c_size_t()
-        st = _lib.get().annety_lhc_verify_host(addr or None, size, self.length_type, self.max_payload, off.ctypes.data,
-                                               ln.ctypes.data, ok.ctypes.data, cap, ctypes.byref(k), ctypes.byref(used))
-        if st < 0:
-            _lib.check(st, "annety_lhc_verify_host")
+        for cap in _frame_caps(size // (self.length_type + 4) + 1, max_frames):
+            off = np.empty(cap, dtype=np.uint64)
+            ln = np.empty(cap, dtype=np.uint32)
+            ok = np.empty(cap, dtype=np.uint8)
+            k, used = ctypes.c_size_t(), ctypes.c_size_t()
+            st = _lib.get().annety_lhc_verify_host(addr or None, size, self.length_type, self.max_payload,
+                                                   off.ctypes.data, ln.ctypes.data, ok.ctypes.data, cap, ctypes.byref(k),
+                                                   ctypes.byref(used))
+            if st < 0:
+                _lib.check(st, "annety_lhc_verify_host")
+            if k.value < cap:
+                break
         n = k.value
         return recv_result(self.length_type, off[:n], ln[:n], int(used.value), st == 1, ok[:n])
 
@@ -254,27 +273,31 @@ class ProtobufCodecFrames(LengthHeaderCodec):
 
     def parse(self, stream: BytesLike, max_frames: int | None = None):
         addr, size, keep = _host_view(stream)
-        cap = size // 8 + 1 if max_frames is None else int(max_frames)
-        off = np.zeros(cap, dtype=np.uint64)
-        ln = np.zeros(cap, dtype=np.uint32)
-        k, used = ctypes.c_size_t(), ctypes.c_size_t()
-        st = _lib.get().annety_pbc_parse(addr or None, size, off.ctypes.data, ln.ctypes.data, cap, ctypes.byref(k),
-                                         ctypes.byref(used))
-        if st < 0:
-            _lib.check(st, "annety_pbc_parse")
+        for cap in _frame_caps(size // 8 + 1, max_frames):
+            off = np.empty(cap, dtype=np.uint64)
+            ln = np.empty(cap, dtype=np.uint32)
+            k, used = ctypes.c_size_t(), ctypes.c_size_t()
+            st = _lib.get().annety_pbc_parse(addr or None, size, off.ctypes.data, ln.ctypes.data, cap, ctypes.byref(k),
+                                             ctypes.byref(used))
+            if st < 0:
+                _lib.check(st, "annety_pbc_parse")
+            if k.value < cap:
+                break
         return off[: k.value], ln[: k.value], int(used.value), st == 1
 
     def decode_host(self, stream: BytesLike, max_frames: int | None = None) -> DecodeResult:
         addr, size, keep = _host_view(stream)
-        cap = size // 8 + 1 if max_frames is None else int(max_frames)
-        off = np.zeros(cap, dtype=np.uint64)
-        ln = np.zeros(cap, dtype=np.uint32)
-        ok = np.zeros(cap, dtype=np.uint8)
-        k, used = ctypes.c_size_t(), ctypes.c_size_t()
-        st = _lib.get().annety_pbc_verify_host(addr or None, size, off.ctypes.data, ln.ctypes.data, ok.ctypes.data, cap,
-                                               ctypes.byref(k), ctypes.byref(used))
-        if st < 0:
-            _lib.check(st, "annety_pbc_verify_host")
+        for cap in _frame_caps(size // 8 + 1, max_frames):
+            off = np.empty(cap, dtype=np.uint64)
+            ln = np.empty(cap, dtype=np.uint32)
+            ok = np.empty(cap, dtype=np.uint8)
+            k, used = ctypes.c_size_t(), ctypes.c_size_t()
+            st = _lib.get().annety_pbc_verify_host(addr or None, size, off.ctypes.data, ln.ctypes.data, ok.ctypes.data,
+                                                   cap, ctypes.byref(k), ctypes.byref(used))
+            if st < 0:
+                _lib.check(st, "annety_pbc_verify_host")
+            if k.value < cap:
+                break
         n = k.value
         return recv_result(self.length_type, off[:n], ln[:n], int(used.value), st == 1, ok[:n])
 

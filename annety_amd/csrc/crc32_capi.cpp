@@ -36,19 +36,65 @@ int hip_fail(hipError_t e) {
     if (e_ != hipSuccess) return hip_fail(e_); \
   } while (0)
 
-// ---------------- host worker pool (staging packs) ----------------
+// ---------------- host worker pools (staging packs, frame walks) ----------------
 // Pageable -> pinned packing is a host memcpy; one thread moves ~10-20 GB/s, below PCIe Gen5 x16, so the
 // pack is split over a small persistent pool (ANNETY_CRC_PACK_THREADS, default min(8, cores)). Several
 // callers may pack at once (the device group's per-device threads, concurrent host batches): each run() is
 // a job in a shared list, the workers take pieces of any job, and every caller also works on its own job
 // until it is done, so concurrent packs share the workers instead of queueing behind one another.
-class PackPool {
+// The frame walks (FrameWalks) use a second pool the same way, started with submit() so that they run
+// while the caller packs; persistent threads, because creating eight threads per call cost milliseconds
+// in a process with a busy address space.
+class WorkPool {
  public:
-  static PackPool& get() {
-    static PackPool pool;
-    return pool;
+  struct Job {
+    std::function<void(size_t)> fn;
+    size_t next = 0, total = 0, left = 0;
+    std::condition_variable done_cv;
+  };
+  WorkPool(int workers) {
+    for (int i = 0; i < workers; i++) workers_.emplace_back([this] { loop(); });
+  }
+  ~WorkPool() {
+    {
+      std::lock_guard<std::mutex> lk(mu_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& w : workers_) w.join();
   }
   int threads() const { return (int)workers_.size() + 1; }
+  // Queues fn(i) for i in [0, n) to the workers; wait() on the returned job.
+  std::unique_ptr<Job> submit(size_t n, std::function<void(size_t)> fn) {
+    auto job = std::make_unique<Job>();
+    job->fn = std::move(fn);
+    job->total = job->left = n;
+    if (n) {
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        jobs_.push_back(job.get());
+      }
+      cv_.notify_all();
+    }
+    return job;
+  }
+  // The caller works on what is left of the job, then waits until the workers' pieces are done.
+  void wait(Job& job) {
+    for (;;) {
+      size_t i;
+      {
+        std::lock_guard<std::mutex> lk(mu_);
+        if (job.next >= job.total) break;
+        i = job.next++;
+      }
+      job.fn(i);
+      finish(job);
+    }
+    std::unique_lock<std::mutex> lk(mu_);
+    job.done_cv.wait(lk, [&] { return job.left == 0; });
+    const auto it = std::find(jobs_.begin(), jobs_.end(), &job);
+    if (it != jobs_.end()) jobs_.erase(it);
+  }
   // Runs fn(i) for i in [0, n) on the pool and the calling thread; returns when all are done.
   template <class F>
   void run(size_t n, F&& fn) {
@@ -57,49 +103,11 @@ class PackPool {
       for (size_t i = 0; i < n; i++) fn(i);
       return;
     }
-    Job job;
-    std::function<void(size_t)> f = fn;
-    job.fn = &f;
-    job.total = job.left = n;
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      jobs_.push_back(&job);
-    }
-    cv_.notify_all();
-    for (;;) {  // the caller works on its own job
-      size_t i;
-      {
-        std::lock_guard<std::mutex> lk(mu_);
-        if (job.next >= job.total) break;
-        i = job.next++;
-      }
-      f(i);
-      finish(job);
-    }
-    std::unique_lock<std::mutex> lk(mu_);
-    job.done_cv.wait(lk, [&] { return job.left == 0; });
-    jobs_.erase(std::find(jobs_.begin(), jobs_.end(), &job));
+    auto job = submit(n, std::function<void(size_t)>(std::ref(fn)));
+    wait(*job);
   }
 
  private:
-  struct Job {
-    std::function<void(size_t)>* fn = nullptr;
-    size_t next = 0, total = 0, left = 0;
-    std::condition_variable done_cv;
-  };
-  PackPool() {
-    int t = (int)std::min<unsigned>(8, std::max<unsigned>(1, std::thread::hardware_concurrency()));
-    if (const char* e = std::getenv("ANNETY_CRC_PACK_THREADS")) t = std::max(1, std::min(64, std::atoi(e)));
-    for (int i = 1; i < t; i++) workers_.emplace_back([this] { loop(); });
-  }
-  ~PackPool() {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    for (auto& w : workers_) w.join();
-  }
   void finish(Job& job) {
     std::lock_guard<std::mutex> lk(mu_);
     if (--job.left == 0) job.done_cv.notify_all();
@@ -124,7 +132,7 @@ class PackPool {
           }
         i = job->next++;
       }
-      (*job->fn)(i);
+      job->fn(i);
       finish(*job);
     }
   }
@@ -135,18 +143,35 @@ class PackPool {
   bool stop_ = false;
 };
 
+int pool_threads(const char* env, int dflt) {
+  int t = dflt;
+  if (const char* e = std::getenv(env)) t = std::max(1, std::min(64, std::atoi(e)));
+  return t;
+}
+WorkPool& pack_pool() {  // the caller is one of the threads
+  static WorkPool pool(pool_threads("ANNETY_CRC_PACK_THREADS",
+                                    (int)std::min<unsigned>(8, std::max<unsigned>(1, std::thread::hardware_concurrency()))) -
+                       1);
+  return pool;
+}
+WorkPool& walk_pool() {  // submitted jobs run on the workers alone until the caller waits
+  static WorkPool pool(pool_threads("ANNETY_CRC_WALK_THREADS",
+                                    (int)std::min<unsigned>(8, std::max<unsigned>(1, std::thread::hardware_concurrency()))));
+  return pool;
+}
+
 // dst[i*dstride, +len) = src[i*sstride, +len) for i < cnt, in parallel pieces of >= 1 MiB.
 void parallel_pack(char* dst, size_t dstride, const char* src, size_t sstride, size_t cnt, size_t len) {
   if (dstride == sstride && dstride == len) {  // one contiguous block
-    const size_t bytes = cnt * len, piece = std::max<size_t>(1 << 20, bytes / (4 * PackPool::get().threads()) + 1);
-    PackPool::get().run((bytes + piece - 1) / piece, [&](size_t i) {
+    const size_t bytes = cnt * len, piece = std::max<size_t>(1 << 20, bytes / (4 * pack_pool().threads()) + 1);
+    pack_pool().run((bytes + piece - 1) / piece, [&](size_t i) {
       const size_t lo = i * piece, hi = std::min(bytes, lo + piece);
       std::memcpy(dst + lo, src + lo, hi - lo);
     });
     return;
   }
   const size_t per = std::max<size_t>(1, (1 << 20) / std::max<size_t>(len, 1));
-  PackPool::get().run((cnt + per - 1) / per, [&](size_t i) {
+  pack_pool().run((cnt + per - 1) / per, [&](size_t i) {
     const size_t lo = i * per, hi = std::min(cnt, lo + per);
     for (size_t k = lo; k < hi; k++) std::memcpy(dst + k * dstride, src + k * sstride, len);
   });
@@ -319,6 +344,11 @@ struct Staging {
   size_t stream_cap = 0;
   char* d_meta = nullptr;  // off (8 B) + len (4 B) + digest (4 B) + ok (1 B) per frame
   size_t meta_cap = 0;     // frames
+  // pinned bounce buffer of that metadata: off + len up, ok down. The runtime's copies from and to the
+  // caller's pageable arrays cost time that grows with the size of the ARRAYS, not of the copy (frame
+  // verify of config 3 through 110 MB output arrays: 28.6 against 49 GiB/s)
+  char* h_meta = nullptr;
+  size_t h_meta_cap = 0;   // frames
 };
 
 struct DeviceCtx {
@@ -960,6 +990,7 @@ int annety_crc_shutdown(void) {
     }
     if (c.stg.d_stream) (void)hipFree(c.stg.d_stream);
     if (c.stg.d_meta) (void)hipFree(c.stg.d_meta);
+    if (c.stg.h_meta) (void)hipHostFree(c.stg.h_meta);
     c.stg = Staging{};
     {
       std::lock_guard<std::mutex> pl(c.pow_mu);
@@ -1382,14 +1413,9 @@ class FrameWalks {
     }
   }
   ~FrameWalks() { join_threads(); }
-  void start(size_t max_threads) {
-    const size_t n = std::min(tasks_.size(), std::max<size_t>(1, max_threads));
-    for (size_t t = 0; t < n; t++)
-      threads_.emplace_back([this] {
-        for (size_t i; (i = next_.fetch_add(1)) < tasks_.size();) run(tasks_[i]);
-      });
-  }
-  void join() {  // idempotent
+  // The walks start on walk_pool()'s workers.
+  void start() { job_ = walk_pool().submit(tasks_.size(), [this](size_t i) { run(tasks_[i]); }); }
+  void join() {  // idempotent; the caller takes any walks still queued
     join_threads();
     if (joined_) return;
     joined_ = true;
@@ -1410,9 +1436,8 @@ class FrameWalks {
       walk_segment(r_, buf(t.c), sizes_[t.c], lo, hi, cap_, segs_[t.c][t.i]);
   }
   void join_threads() {
-    for (auto& th : threads_)
-      if (th.joinable()) th.join();
-    threads_.clear();
+    if (job_) walk_pool().wait(*job_);
+    job_.reset();
   }
   void splice(size_t c) {
     std::vector<ConnWalk>& segs = segs_[c];
@@ -1467,12 +1492,10 @@ class FrameWalks {
   std::vector<std::vector<ConnWalk>> segs_;
   std::vector<ConnWalk> walks_;
   std::vector<Task> tasks_;
-  std::atomic<size_t> next_{0};
-  std::vector<std::thread> threads_;
+  std::unique_ptr<WorkPool::Job> job_;
   bool joined_ = false;
 };
 
-size_t walker_threads() { return std::max(1u, std::min(8u, std::thread::hardware_concurrency())); }
 }  // namespace
 
 static int parse_frames(const FrameRules& r, const void* h_stream, size_t size, uint64_t* payload_off,
@@ -1480,7 +1503,7 @@ static int parse_frames(const FrameRules& r, const void* h_stream, size_t size, 
   if (!n_frames || !consumed || !lhc_type_ok(r.T) || (!h_stream && size) || (max_frames && (!payload_off || !payload_len)))
     return ANNETY_CRC_EINVAL;
   FrameWalks fw(r, &h_stream, &size, 1, max_frames);
-  fw.start(walker_threads());
+  fw.start();
   fw.join();
   const ConnWalk& w = fw.walks()[0];
   std::copy(w.off.begin(), w.off.end(), payload_off);
@@ -1608,6 +1631,16 @@ int annety_pbc_encode_batch(const void* d_src, const uint64_t* d_src_off, const 
 // header walk - a dependent chain of one header read per frame, ~140-170 ns a frame from DRAM - runs on
 // its own walker thread (connections are independent), while the buffers are packed into pinned memory
 // and uploaded (pinned buffers, e.g. annety_crc_host_register'ed NetBuffer arenas, are DMA'd in place).
+// Pageable frame buffers: uploaded by the runtime's own pageable copy (1) or packed into the pinned ring by
+// the pack threads (0, ANNETY_CRC_FRAMES_PACK=1). Read once.
+static bool frames_pageable_direct() {
+  static const bool direct = [] {
+    const char* e = std::getenv("ANNETY_CRC_FRAMES_PACK");
+    return !(e && e[0] == '1');
+  }();
+  return direct;
+}
+
 static int verify_host_iov(const FrameRules& r, const void* const* h_bufs, const size_t* sizes, size_t k,
                            uint64_t* h_payload_off, uint32_t* h_payload_len, uint8_t* h_ok, size_t max_frames,
                            size_t* conn_frames, size_t* conn_consumed, int* conn_rt) {
@@ -1626,7 +1659,7 @@ static int verify_host_iov(const FrameRules& r, const void* const* h_bufs, const
   // the walks (connections, and segments of large buffers, side by side: FrameWalks) run on their own
   // threads while the bytes are packed and uploaded
   FrameWalks fw(r, h_bufs, sizes, k, max_frames);
-  fw.start(walker_threads());
+  fw.start();
   auto join_walkers = [&] { fw.join(); };
   DeviceCtx* c = nullptr;
   int rc = stream_ctx(nullptr, &c);
@@ -1654,7 +1687,7 @@ static int verify_host_iov(const FrameRules& r, const void* const* h_bufs, const
   hipStream_t s = st.stream[0];
   bool pinned = true;
   for (size_t i = 0; i < k && pinned; i++) pinned = !sizes[i] || host_pinned(h_bufs[i], sizes[i]);
-  if (pinned) {
+  if (pinned || frames_pageable_direct()) {
     for (size_t i = 0; i < k; i++) {
       if (!sizes[i]) continue;
       const hipError_t e = hipMemcpyAsync(st.d_stream + base[i], h_bufs[i], sizes[i], hipMemcpyHostToDevice, s);
@@ -1720,26 +1753,35 @@ static int verify_host_iov(const FrameRules& r, const void* const* h_bufs, const
       if (e != hipSuccess) return fail(hip_fail(e));
       st.meta_cap = nf;
     }
+    if (st.h_meta_cap < nf) {
+      if (st.h_meta) (void)hipHostFree(st.h_meta);
+      st.h_meta = nullptr;
+      st.h_meta_cap = 0;
+      const hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&st.h_meta), nf * 13, hipHostMallocDefault);
+      if (e != hipSuccess) return fail(hip_fail(e));
+      st.h_meta_cap = nf;
+    }
     // device offsets are into the concatenation; the host outputs stay relative to each buffer
-    std::vector<uint64_t> goff(nf);
+    uint64_t* m_off = reinterpret_cast<uint64_t*>(st.h_meta);
     for (size_t i = 0, f = 0; i < k; i++)
-      for (size_t q = 0; q < conn_frames[i]; q++, f++) goff[f] = h_payload_off[f] + base[i];
+      for (size_t q = 0; q < conn_frames[i]; q++, f++) m_off[f] = h_payload_off[f] + base[i];
+    std::memcpy(st.h_meta + nf * 8, h_payload_len, nf * 4);
     uint64_t* d_off = reinterpret_cast<uint64_t*>(st.d_meta);
     uint32_t* d_len = reinterpret_cast<uint32_t*>(st.d_meta + nf * 8);
     uint32_t* d_dig = d_len + nf;
     uint8_t* d_ok = reinterpret_cast<uint8_t*>(d_dig + nf);
-    hipError_t e = hipMemcpyAsync(d_off, goff.data(), nf * 8, hipMemcpyHostToDevice, s);
-    if (e == hipSuccess) e = hipMemcpyAsync(d_len, h_payload_len, nf * 4, hipMemcpyHostToDevice, s);
+    hipError_t e = hipMemcpyAsync(d_off, st.h_meta, nf * 12, hipMemcpyHostToDevice, s);  // off then len
     if (e != hipSuccess) return fail(hip_fail(e));
     rc = run_arena(*c, st.d_stream, total, d_off, d_len, nf, d_dig, s, false);
     if (rc == ANNETY_CRC_OK) {
       e = launch_lhc_compare(st.d_stream, d_off, d_len, nf, d_dig, d_ok, s);
-      if (e == hipSuccess) e = hipMemcpyAsync(h_ok, d_ok, nf, hipMemcpyDeviceToHost, s);
+      if (e == hipSuccess) e = hipMemcpyAsync(st.h_meta + nf * 12, d_ok, nf, hipMemcpyDeviceToHost, s);
       if (e != hipSuccess) rc = hip_fail(e);
     }
   }
-  const hipError_t e = hipStreamSynchronize(s);  // also: the offsets' upload has read goff
+  const hipError_t e = hipStreamSynchronize(s);
   if (rc == ANNETY_CRC_OK && e != hipSuccess) rc = hip_fail(e);
+  if (rc == ANNETY_CRC_OK && nf) std::memcpy(h_ok, st.h_meta + nf * 12, nf);
   return rc;
 }
 

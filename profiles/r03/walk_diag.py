@@ -10,10 +10,11 @@ data = torch.randint(0, 256, (int(offs[-1] + lens[-1]),), dtype=torch.uint8, dev
 codec = annety_amd.LengthHeaderCodec(4)
 stream = codec.encode_batch(data, offs.astype(np.uint64), lens.astype(np.uint32)).frames.cpu().numpy()
 payload = float(lens.astype(np.int64).sum())
+CAP = len(lens) + 1 if "cap" in sys.argv[2:] else None
 def rate(buf, reps=5):
-    codec.decode_host(buf)
+    codec.decode_host(buf, max_frames=CAP)
     t0 = time.perf_counter()
-    for _ in range(reps): codec.decode_host(buf)
+    for _ in range(reps): codec.decode_host(buf, max_frames=CAP)
     return payload / ((time.perf_counter() - t0) / reps) / 2 ** 30
 mode = sys.argv[1]
 if mode == "pin_alive":

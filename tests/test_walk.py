@@ -114,3 +114,13 @@ def test_default_segment_matches(small_segments):
     annety_amd.set_walk_segment(0)
     b = LengthHeaderCodec(4).parse(buf)
     assert np.array_equal(a[0], b[0]) and np.array_equal(a[1], b[1]) and a[2:] == b[2:]
+
+
+def test_many_tiny_frames_past_the_first_bound():
+    """Empty payloads (8-byte frames): more frames than the wrapper's first output bound (codec._frame_caps),
+    so the call is repeated with the worst-case bound and still returns every frame."""
+    n = 100_000
+    buf = b"\x00\x00\x00\x04\x00\x00\x00\x00" * n
+    off, ln, used, invalid = LengthHeaderCodec(4).parse(buf)
+    assert off.size == n and int(ln.max()) == 0 and used == len(buf) and not invalid
+    assert np.array_equal(off[:3], np.array([4, 12, 20], dtype=np.uint64))
