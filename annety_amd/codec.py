@@ -18,6 +18,7 @@ There is no CPU fallback: the checksum work runs on the device or the call fails
 from __future__ import annotations
 
 import ctypes
+import threading
 from dataclasses import dataclass
 
 import numpy as np
@@ -68,6 +69,22 @@ def recv_result(length_type: int, off: np.ndarray, ln: np.ndarray, used: int, in
     return DecodeResult(off, ln, used, -1 if invalid else 0, ok)
 
 
+_scratch = threading.local()
+
+
+def _out_arrays(cap: int):
+    """This thread's output arrays for a frame walk of at most `cap` frames (grow-only, reused by every
+    call; the results are copied out of them). Arrays of the bound's size allocated per call cost more than
+    the verify itself on a 1 GiB stream: 110 MB of them, 28 GiB/s against 51 with arrays of the exact frame
+    count."""
+    c = max(int(cap), 1)
+    have = getattr(_scratch, "arrays", None)
+    if have is None or have[0].size < c:
+        have = (np.empty(c, np.uint64), np.empty(c, np.uint32), np.empty(c, np.uint8))
+        _scratch.arrays = have
+    return have[0][:c], have[1][:c], have[2][:c]
+
+
 def _frame_caps(worst: int, max_frames):
     """Output bounds to try in turn. The result arrays are sized by the bound, and worst-case arrays (a
     frame per T + 4 bytes) for a 1 GiB buffer cost more than the verify itself (1.7 GB of fresh arrays per
@@ -88,9 +105,7 @@ def _iov_results(call, name, length_type, streams, max_frames):
     sizes = np.array([v[1] for v in views] or [0], dtype=np.uint64)
     caps = _frame_caps(sum(v[1] // (length_type + 4) + 1 for v in views), max_frames)
     for cap in caps:
-        off = np.empty(max(cap, 1), dtype=np.uint64)
-        ln = np.empty(max(cap, 1), dtype=np.uint32)
-        ok = np.empty(max(cap, 1), dtype=np.uint8)
+        off, ln, ok = _out_arrays(cap)
         nfr = np.zeros(max(k, 1), dtype=np.uint64)
         used = np.zeros(max(k, 1), dtype=np.uint64)
         rts = np.zeros(max(k, 1), dtype=np.int32)
@@ -99,6 +114,8 @@ def _iov_results(call, name, length_type, streams, max_frames):
         _lib.check(st, name)
         if int(nfr[:k].sum()) < cap:
             break
+    total = int(nfr[:k].sum())
+    off, ln, ok = off[:total].copy(), ln[:total].copy(), ok[:total].copy()
     out, pos = [], 0
     for c in range(k):
         n = int(nfr[c])
@@ -132,8 +149,7 @@ class LengthHeaderCodec:
         stopped_on_invalid_length)."""
         addr, size, keep = _host_view(stream)
         for cap in _frame_caps(size // (self.length_type + 4) + 1, max_frames):
-            off = np.empty(cap, dtype=np.uint64)
-            ln = np.empty(cap, dtype=np.uint32)
+            off, ln, _ = _out_arrays(cap)
             k, used = ctypes.c_size_t(), ctypes.c_size_t()
             st = _lib.get().annety_lhc_parse(addr or None, size, self.length_type, self.max_payload, off.ctypes.data,
                                              ln.ctypes.data, cap, ctypes.byref(k), ctypes.byref(used))
@@ -141,7 +157,7 @@ class LengthHeaderCodec:
                 _lib.check(st, "annety_lhc_parse")
             if k.value < cap:
                 break
-        return off[: k.value], ln[: k.value], int(used.value), st == 1
+        return off[: k.value].copy(), ln[: k.value].copy(), int(used.value), st == 1
 
     def verify(self, d_stream, d_off, d_len, out_ok=None, out_digest=None, stream=None, arena=True):
         """Device checksum check of located frames: ok uint8[n] (1 = trailer matches).
@@ -191,9 +207,7 @@ class LengthHeaderCodec:
         overlaps the stream's copy to the current device, the CRCs are checked there."""
         addr, size, keep = _host_view(stream)
         for cap in _frame_caps(size // (self.length_type + 4) + 1, max_frames):
-            off = np.empty(cap, dtype=np.uint64)
-            ln = np.empty(cap, dtype=np.uint32)
-            ok = np.empty(cap, dtype=np.uint8)
+            off, ln, ok = _out_arrays(cap)
             k, used = ctypes.c_size_t(), ctypes.c_size_t()
             st = _lib.get().annety_lhc_verify_host(addr or None, size, self.length_type, self.max_payload,
                                                    off.ctypes.data, ln.ctypes.data, ok.ctypes.data, cap, ctypes.byref(k),
@@ -203,7 +217,7 @@ class LengthHeaderCodec:
             if k.value < cap:
                 break
         n = k.value
-        return recv_result(self.length_type, off[:n], ln[:n], int(used.value), st == 1, ok[:n])
+        return recv_result(self.length_type, off[:n].copy(), ln[:n].copy(), int(used.value), st == 1, ok[:n].copy())
 
     def decode_host_iov(self, streams, max_frames: int | None = None) -> list:
         """Codec::recv over K connections' receive buffers in one call (annety_lhc_verify_host_iov): one
@@ -274,8 +288,7 @@ class ProtobufCodecFrames(LengthHeaderCodec):
     def parse(self, stream: BytesLike, max_frames: int | None = None):
         addr, size, keep = _host_view(stream)
         for cap in _frame_caps(size // 8 + 1, max_frames):
-            off = np.empty(cap, dtype=np.uint64)
-            ln = np.empty(cap, dtype=np.uint32)
+            off, ln, _ = _out_arrays(cap)
             k, used = ctypes.c_size_t(), ctypes.c_size_t()
             st = _lib.get().annety_pbc_parse(addr or None, size, off.ctypes.data, ln.ctypes.data, cap, ctypes.byref(k),
                                              ctypes.byref(used))
@@ -283,14 +296,12 @@ class ProtobufCodecFrames(LengthHeaderCodec):
                 _lib.check(st, "annety_pbc_parse")
             if k.value < cap:
                 break
-        return off[: k.value], ln[: k.value], int(used.value), st == 1
+        return off[: k.value].copy(), ln[: k.value].copy(), int(used.value), st == 1
 
     def decode_host(self, stream: BytesLike, max_frames: int | None = None) -> DecodeResult:
         addr, size, keep = _host_view(stream)
         for cap in _frame_caps(size // 8 + 1, max_frames):
-            off = np.empty(cap, dtype=np.uint64)
-            ln = np.empty(cap, dtype=np.uint32)
-            ok = np.empty(cap, dtype=np.uint8)
+            off, ln, ok = _out_arrays(cap)
             k, used = ctypes.c_size_t(), ctypes.c_size_t()
             st = _lib.get().annety_pbc_verify_host(addr or None, size, off.ctypes.data, ln.ctypes.data, ok.ctypes.data,
                                                    cap, ctypes.byref(k), ctypes.byref(used))
@@ -299,7 +310,7 @@ class ProtobufCodecFrames(LengthHeaderCodec):
             if k.value < cap:
                 break
         n = k.value
-        return recv_result(self.length_type, off[:n], ln[:n], int(used.value), st == 1, ok[:n])
+        return recv_result(self.length_type, off[:n].copy(), ln[:n].copy(), int(used.value), st == 1, ok[:n].copy())
 
     def decode_host_iov(self, streams, max_frames: int | None = None) -> list:
         lib = _lib.get()
