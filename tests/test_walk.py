@@ -124,3 +124,29 @@ def test_many_tiny_frames_past_the_first_bound():
     off, ln, used, invalid = LengthHeaderCodec(4).parse(buf)
     assert off.size == n and int(ln.max()) == 0 and used == len(buf) and not invalid
     assert np.array_equal(off[:3], np.array([4, 12, 20], dtype=np.uint64))
+
+
+def test_concurrent_parses_share_the_walk_pool(small_segments):
+    """Several threads parsing at once: their segment walks share the persistent walk pool (each caller
+    also takes its own queued walks), and every result equals the sequential walk."""
+    import threading
+
+    bufs = [make_stream(20 + i, 4, 800, 6000) for i in range(6)]
+    want = [ref_walk(b, 4, 4, 64 << 20, len(b)) for b in bufs]
+    errors = []
+
+    def work(i):
+        try:
+            for _ in range(3):
+                off, ln, used, invalid = LengthHeaderCodec(4).parse(bufs[i])
+                w = want[i]
+                assert np.array_equal(off, np.array(w[0], dtype=np.uint64)) and (used, invalid) == (w[2], w[3])
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errors.append(e)
+
+    threads = [threading.Thread(target=work, args=(i,)) for i in range(len(bufs))]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert not errors, errors
