@@ -4,15 +4,11 @@
 BASELINE.json metric: "CRC-32C GiB/s device-resident (1M x 1KiB) @1/2/4/8 MI355X; % HBM roofline".
 A step = one pass of the hot path over the GPU's batch, already resident in HBM.
 
-  * Default, any N: BASELINE config 1 per GPU, 1M x 1 KiB resident in each GPU's HBM, one batch
-    launch per step, weak scaling: the N = 1, 2, 4, 8 lines run the same per-GPU workload, so they are
-    points of one curve (`config.workload` is identical at every N). At N > 1 each step's digests also
-    travel to rank 0 over RCCL/xGMI (annety_amd.sharded.PipelinedGather; step s's gather overlaps step
-    s+1's kernel) and that gather is inside `value`; `value_compute_only` is the same step without it.
-  * --strong: the same 1M x 1 KiB TOTAL split N ways (contiguous shards), `"scaling": "strong"`
-    (SURVEY.md §8e).
-  * --config 4: BASELINE config 4's per-GPU shard, 8M x 1 KiB (8 GiB) per rank, checksummed in chunks
-    whose digests are gathered while the next chunk computes.
+  * N = 1 (default): BASELINE config 1, 1M x 1 KiB, one batch launch per step.
+  * N > 1: BASELINE config 4's per-GPU shard, 8M x 1 KiB (8 GiB) per rank, weak scaling. A step
+    checksums the shard in chunks and gathers each chunk's digests to rank 0 over RCCL/xGMI while
+    the next chunk is computed (annety_amd.sharded.PipelinedGather) - the gather is inside `value`;
+    `value_compute_only` is the same step without it.
   * --config 2 / 3 run the other single-GPU configs (4K x 4 MiB; Zipf 64 B-64 KiB packed, arena path)
     as secondary lines.
 
@@ -21,7 +17,7 @@ process per GPU, RANK/LOCAL_RANK/WORLD_SIZE/MASTER_ADDR=127.0.0.1), before anyth
 under torch.distributed.run it uses the launcher's ranks. Prints ONE JSON line on rank 0
 (contract: DESIGN.md §4).
 
-Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C] [--strong] [--e2e] [--no-cpu]
+Usage:  python bench.py [--gpus N] [--steps K] [--warmup W] [--config C] [--e2e] [--no-cpu]
 """
 from __future__ import annotations
 
@@ -41,8 +37,8 @@ sys.path.insert(0, ROOT)
 METRIC = "CRC-32C GiB/s device-resident (1M×1KiB) @1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md (8.0 TB/s)
 # Per-launch HBM bytes measured by profiles/pmc.sh at this code (FETCH_SIZE x2 + WRITE_SIZE), per config.
-PMC_FILES = {1: "profiles/r03/config1_pmc.json", 3: "profiles/r03/config3_pmc.json",
-             2: "profiles/r03/config2_pmc.json", 4: "profiles/r03/config1_pmc.json"}
+PMC_FILES = {1: "profiles/r02/config1_pmc.json", 3: "profiles/r02/config3_pmc.json",
+             2: "profiles/r02/config2_pmc.json", 4: "profiles/r02/config1_pmc.json"}
 # The reference build of oracle/_ref (oracle/Makefile): the reference's Release flags without -march=native.
 REF_FLAGS = "g++ -std=c++11 -O2 -DNDEBUG (CMakeLists.txt:24,48 Release flags; -march=native dropped so the .so runs on any host)"
 
@@ -54,20 +50,15 @@ def parse():
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--prewarm-s", type=float, default=1.0,
                    help="untimed seconds of launches before warmup (the GPU ramps its clocks on sustained load)")
-    p.add_argument("--config", type=int, default=1, choices=[1, 2, 3, 4],
-                   help="BASELINE config: 1 = 1M x 1 KiB per GPU (default at every N), 2 = 4K x 4 MiB, "
-                        "3 = Zipf 64 B-64 KiB (~1 GiB), 4 = 8M x 1 KiB per GPU (config 4's shard) in chunks")
-    p.add_argument("--strong", action="store_true",
-                   help="fixed configs: --payloads (default 1M) is the TOTAL over all ranks, split into contiguous "
-                        "shards (strong scaling); default is per GPU (weak scaling)")
-    p.add_argument("--var-path", choices=["arena", "auto", "sorted"], default="arena",
+    p.add_argument("--config", type=int, default=None, choices=[1, 2, 3, 4],
+                   help="BASELINE config: 1 = 1M x 1 KiB (N=1 default), 2 = 4K x 4 MiB, 3 = Zipf 64 B-64 KiB (~1 GiB), "
+                        "4 = 8M x 1 KiB per GPU + pipelined RCCL gather (N>1 default)")
+    p.add_argument("--var-path", choices=["arena", "sorted"], default="arena",
                    help="config 3: arena = one pass over the packed arena + per-payload stitch (annety_crc32_batch_var_arena); "
-                        "auto = annety_crc32_batch_var, which picks the arena path itself from the batch's recorded extent; "
-                        "sorted = the length-bucketed path only (ANNETY_CRC_VAR_AUTO=0)")
-    p.add_argument("--chunks", type=int, default=None,
-                   help="N>1: chunks per shard for the pipelined gather (default 1 for config 1: step s's gather "
-                        "overlaps step s+1's kernel; 2 for config 4, one-rank rehearsal 1/2/4 chunks "
-                        "5755-5770/5748/5613-5616 GiB/s, profiles/r02/config4_chunks_overlap.log)")
+                        "sorted = the general length-bucketed path (annety_crc32_batch_var)")
+    p.add_argument("--chunks", type=int, default=2,
+                   help="config 4: chunks per shard for the pipelined gather (one-rank rehearsal with the cross-step "
+                        "overlap, one box: 1/2/4 chunks 5755-5770/5748/5613-5616 GiB/s, profiles/r02/config4_chunks_overlap.log)")
     p.add_argument("--hw-queues", type=int, default=8,
                    help="N>1: raise GPU_MAX_HW_QUEUES to this (<= 32) so the compute and RCCL streams get queues of "
                         "their own")
@@ -78,10 +69,6 @@ def parse():
                    help="config 4: wait for a step's gathers before the next step starts (default: the digests "
                         "alternate between two buffers and step s+1's chunks compute while step s's last gathers "
                         "are in flight; every gather is still inside the timed region)")
-    p.add_argument("--gather-buffers", type=int, default=2,
-                   help="N>1: digest buffers the steps rotate through; step s+1 computes while step s's gather is in "
-                        "flight, and the compute stream waits for step s's gather only before step s+buffers reuses "
-                        "its buffer (1 = wait for every step's gather before the next step)")
     p.add_argument("--dist", action="store_true",
                    help="run the N>1 code path (RCCL process group, pipelined digest gather, gather check, max over "
                         "ranks) even at one rank: a one-GPU rehearsal of the multi-GPU run")
@@ -90,8 +77,7 @@ def parse():
                         "(annety_crc_reserve_cus; default 8 when gathering, else 0)")
     p.add_argument("--compute-stream", choices=["default", "own"], default="default",
                    help="launch the checksum kernels on torch's default stream or on a stream of their own")
-    p.add_argument("--payloads", type=int, default=None,
-                   help="override payloads per GPU (fixed configs; with --strong, the total over all ranks)")
+    p.add_argument("--payloads", type=int, default=None, help="override payloads per GPU (fixed configs)")
     p.add_argument("--len", type=int, default=None, help="override payload bytes (fixed configs)")
     p.add_argument("--e2e", action="store_true",
                    help="also time the host-memory path (pinned staging, H2D -> kernel -> D2H) on the same batch")
@@ -166,7 +152,7 @@ def zipf_batch(seed: int, target: int = 1 << 30):
 class Workload:
     """One batch resident on the device plus everything the report needs about it."""
 
-    def __init__(self, args, dev, rank, world=1):
+    def __init__(self, args, dev, rank):
         import torch
 
         self.torch = torch
@@ -179,13 +165,6 @@ class Workload:
             default_n = {1: 1 << 20, 2: 4096, 4: 8 << 20}[args.config]
             n = args.payloads or default_n
             L = args.len or (4 << 20 if args.config == 2 else 1024)
-            self.n_total = n * world  # payloads over all ranks
-            if args.strong:  # n is the job's total: this rank's contiguous shard of it
-                from annety_amd.sharded import shard_range
-
-                self.n_total = n
-                lo, hi = shard_range(n, rank, world)
-                n = hi - lo
             self.n, self.L = n, L
             self.data = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=dev, generator=gen)
             self.payload_bytes = n * L
@@ -195,15 +174,13 @@ class Workload:
                 self.kernel = "crc32_fixed_kernel<32> over 64 KiB segments + crc32_split_join (annety_amd/csrc/crc32_kernels.hip)"
             else:
                 self.kernel = "crc32_oneround_kernel<8> (annety_amd/csrc/crc32_kernels.hip)"
-            # the workload only: identical at every N for a weak-scaling run, so the driver's N = 1..8 lines
-            # are one curve (the gather, when there is one, is described in the line's "gather" object)
-            if args.strong:
-                self.desc = (f"BASELINE config {args.config}, strong scaling: {self.n_total} x {L} B payloads in total, "
-                             f"contiguous shards of {self.n_total // world}-{-(-self.n_total // world)} payloads per GPU, "
-                             "one batch launch per step")
-            elif args.config == 4:
-                self.desc = (f"BASELINE config 4 shard: {n} x {L} B payloads contiguous in HBM per GPU "
-                             "(64M x 1 KiB at 8 GPUs), checksummed in chunks per step")
+            if args.config == 4:
+                self.desc = (f"BASELINE config 4 shard: {n} x {L} B payloads per GPU (64M x 1 KiB at 8 GPUs), "
+                             f"{args.chunks} chunks per step (the last cut into {args.taper} halving pieces), each chunk's "
+                             "digests gathered to rank 0 over RCCL "
+                             "while the next chunk is computed" +
+                             ("" if args.no_overlap_steps else
+                              " (digests double-buffered: the next step computes while this step's last gathers finish)"))
             else:
                 self.desc = (f"BASELINE config {args.config}: {n} x {L} B payloads contiguous in HBM per GPU, "
                              "one batch launch per step")
@@ -211,47 +188,27 @@ class Workload:
             lens, offs = zipf_batch(0x5EED + rank)
             total = int(lens.sum())
             self.n, self.L = len(lens), None
-            self.n_total = self.n * world
             self.data = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=gen)
             self.offsets = torch.from_numpy(offs).to(dev)
             self.lengths = torch.from_numpy(lens.astype(np.int32)).to(dev)
             self.payload_bytes = total
             self.algo_bytes = total + 4 * self.n + 12 * self.n  # + offset/length metadata reads
             self.arena = args.var_path == "arena"
-            self.var_path = args.var_path
             self.kernel = ("crc32_arena_lines_kernel + crc32_arena_stitch_kernel, one step "
                            "(annety_amd/csrc/crc32_arena.hip, crc32_arena_lines.h)" if self.arena else
-                           "crc32_extent_kernel + (arena or sorted path, chosen per call), one step "
-                           "(annety_amd/csrc/crc32_capi.cpp run_var_auto)" if args.var_path == "auto" else
-                           "crc32_extent_kernel<count> + crc32_bucket_place + crc32_var_kernel<32/16/4>, one step "
-                           "(annety_amd/csrc/crc32_arena.hip, crc32_kernels.hip)")
+                           "crc32_bucket_hist/scan/scatter + crc32_var_kernel<32/8/2>, one step "
+                           "(annety_amd/csrc/crc32_kernels.hip)")
             self.desc = (f"BASELINE config 3: {self.n} payloads, Zipf(1.1) lengths 64 B-64 KiB packed unaligned, "
-                         f"{total / 2**30:.3f} GiB per GPU, " + {"arena": "arena path", "auto": "automatic path choice",
-                                                                  "sorted": "sorted path"}[args.var_path])
-        # strong scaling: shards differ by at most one payload; the digest buffer is padded (zeros) to the
-        # largest so that every rank's gather moves the same count
-        self.n_pad = -(-self.n_total // world) if getattr(args, "strong", False) else self.n
-        self.out = torch.zeros(self.n_pad, dtype=torch.int32, device=dev)
-        from annety_amd import _lib
-
-        self._fixed = _lib.get().annety_crc32_batch_fixed
-        self._data_ptr = self.data.data_ptr()
+                         f"{total / 2**30:.3f} GiB per GPU, " + ("arena path" if self.arena else "sorted path"))
+        self.out = torch.empty(self.n, dtype=torch.int32, device=dev)
 
     def launch(self, stream_handle, lo: int = 0, hi: int | None = None):
         """Digests of payloads [lo, hi) into self.out[lo:hi] (fixed configs); the whole batch otherwise."""
         import annety_amd
-        from annety_amd import _lib
 
         if self.config in (1, 2, 4):
-            hi = self.n_pad if hi is None else hi
-            top = min(hi, self.n)  # the padding past this rank's shard (strong scaling) stays zero
-            if top > lo:
-                # the C-ABI call itself (annety_amd.crc32_batch's checks done once in __init__): a step is
-                # 0.17 ms, and per-call Python checks would eat into the launch rate on a slow host
-                st = self._fixed(self._data_ptr + lo * self.L, top - lo, self.L, self.L,
-                                 self.out.data_ptr() + 4 * lo, stream_handle)
-                if st:
-                    _lib.check(st, "annety_crc32_batch_fixed")
+            hi = self.n if hi is None else hi
+            annety_amd.crc32_batch(self.data[lo * self.L:], hi - lo, self.L, out=self.out[lo:hi], stream=stream_handle)
             return self.out[lo:hi]
         annety_amd.crc32_batch_var(self.data, self.offsets, self.lengths, out=self.out, stream=stream_handle,
                                    arena=True if self.arena else None)
@@ -321,14 +278,6 @@ def cpu_baseline(h: np.ndarray, offs: np.ndarray, lens: np.ndarray, budget_s: fl
 
         def run(th):
             oracle.batch_fixed_mt(h, n, L0, threads=th)
-    elif oracle.ref_available():
-        lib, kind = oracle.ref_lib(), "reference"
-        out = np.zeros(n, dtype=np.uint32)
-        offs_c = np.ascontiguousarray(offs, dtype=np.uint64)
-        lens_c = np.ascontiguousarray(lens, dtype=np.uint32)
-
-        def run(th):  # threads balanced by bytes (oracle/ref_wrapper.cc)
-            lib.ref_crc32_batch_var_mt(h.ctypes.data, offs_c.ctypes.data, lens_c.ctypes.data, n, out.ctypes.data, th)
     else:
         kind = "port"
 
@@ -419,32 +368,17 @@ def e2e_host_path(w: Workload):
         out = {}
         res["frames_pageable"], res["frames_pageable_ms"] = rate(lambda: out.__setitem__("p", codec.decode_host(stream)),
                                                                  w.payload_bytes)
-        # the same with the header walk done whole, one frame after another (no segmented speculative walks)
-        annety_amd.set_walk_segment(1 << 40)
-        res["frames_pageable_whole_walk"], _ = rate(lambda: codec.decode_host(stream), w.payload_bytes)
-        annety_amd.set_walk_segment(0)
         pin = annety_amd.PinnedHostBuffer(stream.size)
         pin.array[:] = stream
         res["frames_pinned"], res["frames_pinned_ms"] = rate(lambda: out.__setitem__("q", codec.decode_host(pin.array)),
                                                              w.payload_bytes)
         pin.close()
-        # the same frames as K connections' receive buffers (one NetBuffer per TcpConnection), verified in one
-        # call (annety_lhc_verify_host_iov): the K header walks run side by side
-        kconn = 16
-        cuts = np.linspace(0, len(lens), kconn + 1).astype(np.int64)
-        fstart = np.concatenate([[0], np.cumsum(lens.astype(np.int64) + 8)])  # T = 4 + trailer 4
-        conns = [stream[int(fstart[cuts[i]]):int(fstart[cuts[i + 1]])].copy() for i in range(kconn)]
-        res[f"frames_iov{kconn}_pageable"], res[f"frames_iov{kconn}_pageable_ms"] = rate(
-            lambda: out.__setitem__("v", codec.decode_host_iov(conns)), w.payload_bytes)
-        iov_ok = all(bool(r.ok.all()) and r.rt == 0 for r in out["v"]) and sum(int(r.ok.size) for r in out["v"]) == len(lens)
         r = out["p"]
         res["frames"] = int(r.ok.size)
-        res["all_frames_verified"] = bool(r.ok.all() and out["q"].ok.all() and r.rt == 0 and r.consumed == stream.size
-                                          and iov_ok)
+        res["all_frames_verified"] = bool(r.ok.all() and out["q"].ok.all() and r.rt == 0 and r.consumed == stream.size)
         res["stream_bytes"] = int(stream.size)
-        res["path"] = ("LengthHeaderCodec stream in host memory -> header walk (host threads, segments walked side "
-                       "by side from speculative entries) || staged H2D -> arena verify on the device -> per-frame "
-                       "verdicts D2H")
+        res["path"] = ("LengthHeaderCodec stream in host memory -> header walk (host thread) || staged H2D -> "
+                       "arena verify on the device -> per-frame verdicts D2H")
         return res
     return None
 
@@ -456,12 +390,8 @@ def main():
         return spawn(args.gpus)  # before anything touches the GPU
     world = max(world, 1)
     multi = world > 1 or args.dist  # the distributed code path
-    if args.strong and args.config not in (1, 4):
-        raise SystemExit("--strong applies to the fixed 1 KiB configs (1, 4)")
-    if args.chunks is None:
-        args.chunks = 2 if args.config == 4 else 1
-    if args.var_path == "sorted":
-        os.environ["ANNETY_CRC_VAR_AUTO"] = "0"  # read once by the library: before it loads
+    if args.config is None:
+        args.config = 4 if multi else 1
     if multi and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < args.hw_queues:
         # HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default); the compute stream, torch's
         # RCCL stream and RCCL's own streams then share queues, and a queue runs its packets in order. Set
@@ -491,30 +421,26 @@ def main():
     # the checksum kernels take one workgroup per CU; with the gather overlapped on another stream, a few
     # free CUs let the RCCL kernels run beside them instead of between chunks
     annety_amd.reserve_cus(args.reserve_cus if args.reserve_cus is not None else (8 if multi else 0))
-    w = Workload(args, dev, rank, world)
+    w = Workload(args, dev, rank)
     if args.compute_stream == "own":
         torch.cuda.set_stream(torch.cuda.Stream(dev))
     stream = torch.cuda.current_stream(dev)
     sh = int(stream.cuda_stream)
-    # strong scaling: shards differ by at most one payload; every rank gathers a buffer of the largest
-    nbuf = 1 if (not multi or args.no_overlap_steps) else max(1, args.gather_buffers)
-    pipe = (sharded.PipelinedGather(w.n_pad, args.chunks, dst=0, device=dev, taper=args.taper, buffers=nbuf)
-            if multi else None)
+    pipe = sharded.PipelinedGather(w.n, args.chunks, dst=0, device=dev, taper=args.taper) if multi else None
 
     # N>1: the digests alternate between two buffers, so step s+1's chunks can be computed while step s's
     # last gathers still read the other buffer; a step's handles are waited (the compute stream waits for
     # its gathers, no host block) after the next step is launched, before the buffer comes round again
-    outs = [w.out] + [torch.zeros_like(w.out) for _ in range(nbuf - 1)]
+    outs = [w.out, torch.empty_like(w.out)] if (pipe is not None and not args.no_overlap_steps) else [w.out]
     nstep = [0]
 
     def step(gather: bool = True):
         if pipe is None:
             w.launch(sh)
             return []
-        b = nstep[0] % len(outs)
-        w.out = outs[b]
+        w.out = outs[nstep[0] % len(outs)]
         nstep[0] += 1
-        return pipe.run(lambda lo, hi: w.launch(sh, lo, hi), gather=gather, buf=b)
+        return pipe.run(lambda lo, hi: w.launch(sh, lo, hi), gather=gather)
 
     def produce(s: int, lo: int, hi: int):
         w.out = outs[s % len(outs)]
@@ -541,22 +467,12 @@ def main():
     if gather_ok is False:
         raise SystemExit(f"rank {rank}: gathered digests differ from the ranks' own")
 
-    def timed(steps: int, gather: bool, groups: int = 1):
-        """K steps bracketed by a barrier + synchronise on both sides; max over ranks. HIP events on the
-        launch stream inside the same bracket give the kernel-stream time (the roofline's launch duration);
-        with groups > 1, per-group events give a per-step median / min / max (not with the gather on: its
-        stream waits would cut across group boundaries)."""
-        ngroups = max(1, min(groups, steps)) if (pipe is None or not gather) else 1
-        gsteps = [steps * (i + 1) // ngroups - steps * i // ngroups for i in range(ngroups)]
-        evs = [torch.cuda.Event(enable_timing=True) for _ in range(ngroups + 1)]
+    def timed(steps: int, gather: bool) -> float:
         if multi:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        evs[0].record(stream)
-        for i, gs in enumerate(gsteps):
-            run_steps(gs, gather)
-            evs[i + 1].record(stream)
+        run_steps(steps, gather)
         torch.cuda.synchronize()
         if multi:
             dist.barrier()
@@ -565,9 +481,7 @@ def main():
             t = torch.tensor([el], dtype=torch.float64, device=dev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             el = float(t.item())
-        kern = evs[0].elapsed_time(evs[-1]) / steps
-        per = sorted(evs[i].elapsed_time(evs[i + 1]) / gs for i, gs in enumerate(gsteps))
-        return el, kern, per
+        return el
 
     t_pw = time.perf_counter()
     while time.perf_counter() - t_pw < args.prewarm_s:
@@ -577,27 +491,22 @@ def main():
     run_steps(args.warmup, True)
     torch.cuda.synchronize()
 
-    # the timed region carries two events only (an event between two launches is a marker in the queue)
-    elapsed, kern_ms, _ = timed(args.steps, gather=True)
-    compute_only = None
-    if multi:  # the same steps without the gather: value_compute_only, and the roofline's kernel time
-        compute_only, kern_ms, _ = timed(args.steps, gather=False)
-    # per-step spread: the same number of steps again, events around groups of steps (up to 20 groups)
-    _, _, per_step = timed(args.steps, gather=False, groups=20)
-    kern_median = float(np.median(per_step))
-    ngroups = len(per_step)
+    # kernel-only time on the launch stream (HIP events around the same number of steps, no gather)
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step(gather=False)
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    kern_ms = ev0.elapsed_time(ev1) / args.steps
+
+    elapsed = timed(args.steps, gather=True)
+    compute_only = timed(args.steps, gather=False) if multi else None
 
     if rank == 0:
-        # every rank's payload bytes (weak: n per GPU x world; strong: the fixed total)
-        total_gib = (w.n_total * w.L if w.L else w.payload_bytes * world) * args.steps / 2 ** 30
+        total_gib = w.payload_bytes * world * args.steps / 2 ** 30
         achieved = w.algo_bytes / (kern_ms / 1e3) / 1e9
-        if args.config == 1:
-            metric = METRIC if not args.strong else METRIC.replace("(1M×1KiB)", "(1M×1KiB total, strong scaling)")
-        elif args.config == 4:
-            metric = METRIC.replace("(1M×1KiB)", "(8M×1KiB per GPU, config 4)" if not args.strong
-                                    else "(8M×1KiB total, config 4, strong scaling)")
-        else:
-            metric = METRIC.replace("(1M×1KiB)", f"(config {args.config})")
+        metric = METRIC if args.config in (1, 4) else METRIC.replace("(1M×1KiB)", f"(config {args.config})")
         line = {
             "metric": metric,
             "value": round(total_gib / elapsed, 2),
@@ -606,20 +515,14 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            # kernel-stream time per step (HIP events, no gather) over up to 20 consecutive groups of steps, in a
-            # pass of its own right after the timed region
-            "ms_per_step_median": round(kern_median, 4),
-            "ms_per_step_min": round(per_step[0], 4),
-            "ms_per_step_max": round(per_step[-1], 4),
             "higher_is_better": True,
-            "scaling": "strong" if args.strong else "weak",
+            "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u32",
             "data": "synthetic (torch.randint bytes on device, seeded per rank)",
             "config": {
                 "workload": w.desc,
                 "payloads_per_gpu": w.n,
-                "payloads_total": w.n_total,
                 "payload_bytes": w.L if w.L else "zipf",
                 "bytes_per_gpu": w.payload_bytes,
                 "parallelism": f"shard{world}" if multi else "single",
@@ -633,8 +536,6 @@ def main():
                 "traffic": pmc_traffic(w, args.var_path),
                 "kernel": w.kernel,
                 "kernel_ms_avg": round(kern_ms, 4),
-                "kernel_ms_median": round(kern_median, 4),
-                "timing_groups": ngroups,
                 "algorithmic_bytes_per_launch": w.algo_bytes,
             },
             "cpu_baseline": None if (args.no_cpu or multi) else cpu_baseline(hs, ho, hl, args.cpu_seconds),
@@ -643,8 +544,7 @@ def main():
         if multi:
             line["rccl_ranks"] = dist.get_world_size()
             line["backend"] = dist.get_backend()
-            line["gather"] = {"what": "every rank's digests to rank 0 (RCCL gather over xGMI), inside `value`",
-                              "chunks": len(pipe.bounds), "bytes_to_rank0_per_step": 4 * w.n_pad * (world - 1),
+            line["gather"] = {"chunks": len(pipe.bounds), "bytes_to_rank0_per_step": 4 * w.n * (world - 1),
                               "verified": bool(gather_ok), "overlapped_with_compute": True,
                               "overlapped_across_steps": len(outs) > 1}
             line["value_compute_only"] = round(total_gib / compute_only, 2)
