@@ -307,6 +307,9 @@ __global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __rest
   //          loads     (dec1, r1) = step q+1, decoded from the descriptor fetched at q-1,
   //          fetches   the raw descriptor of step q+2's task.
   size_t t0 = t_begin + gid;
+  // a block with no task (an empty length class of the sorted path, or fewer tasks than lane groups)
+  // leaves before its first descriptor load and the image staging
+  if (!__syncthreads_or(t0 < t_end)) return;
   VarTask dec0 = decode_task<G>(raw(t0), t0 < t_end);
   if constexpr (UPD) dec0.state = dec0.valid ? out[dec0.p] : 0u;
   uint32_t r0 = 0;
