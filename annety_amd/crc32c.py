@@ -103,13 +103,14 @@ def scratch_stats(device: int = 0) -> dict:
 
 
 def var_path_stats(device: int = 0) -> dict:
-    """annety_crc_var_path_stats: how many automatic variable-batch calls took the arena / sorted path."""
+    """annety_crc_var_path_stats: how many automatic variable-batch calls took the arena / sorted path, and
+    how many of the arena calls ran without recording their extent ("arena_unrecorded")."""
     import ctypes
 
-    a, b = ctypes.c_uint64(), ctypes.c_uint64()
-    _lib.check(_lib.get().annety_crc_var_path_stats(int(device), ctypes.byref(a), ctypes.byref(b)),
+    a, b, u = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    _lib.check(_lib.get().annety_crc_var_path_stats(int(device), ctypes.byref(a), ctypes.byref(b), ctypes.byref(u)),
                "annety_crc_var_path_stats")
-    return {"arena": a.value, "sorted": b.value}
+    return {"arena": a.value, "sorted": b.value, "arena_unrecorded": u.value}
 
 
 def stream_release(stream) -> None:

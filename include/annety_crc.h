@@ -77,8 +77,9 @@ int annety_crc_stream_release(void* stream);
  * slot between streams so far, device-wide synchronisations so far (0 outside annety_crc_shutdown). */
 int annety_crc_scratch_stats(int device, uint64_t* slots, uint64_t* handoffs, uint64_t* device_syncs);
 /* Calls of annety_crc32_batch_var / annety_crc32_update_batch_var on `device` (n >= 1024) that took the
- * arena path and the sorted path so far (the automatic choice; test and tuning visibility). */
-int annety_crc_var_path_stats(int device, uint64_t* arena, uint64_t* sorted);
+ * arena path and the sorted path so far (the automatic choice; test and tuning visibility), and how many
+ * of the arena calls ran without recording their extent (between two recording calls). Any may be NULL. */
+int annety_crc_var_path_stats(int device, uint64_t* arena, uint64_t* sorted, uint64_t* arena_unrecorded);
 
 /* ---- host scalar API: exact replacements of the reference's inline methods ----
  * annety_crc32_long   replaces Crc32c::crc32_long(const char*, size_t)   include/Crc32c.h:58-69

@@ -96,7 +96,7 @@ def test_layout_changes_under_the_same_pointers(gpu):
         o.copy_(torch.from_numpy(v))  # same pointers, new layout
         annety_amd.crc32_batch_var(d, o, ln, out=out)
         _check(out, data, v, lens)
-    assert annety_amd.var_path_stats(0)["arena"] > a0  # the first changed call still took the (checked) arena path
+    assert annety_amd.var_path_stats(0)["arena"] > a0  # the first changed call still took the arena path
 
 
 def test_update_mode_auto(gpu):
@@ -146,3 +146,31 @@ def test_sorted_calls_back_to_back(gpu):
         _check(out, data, offs, lens)
     s1 = annety_amd.var_path_stats(0)
     assert s1["arena"] == s0["arena"] and s1["sorted"] - s0["sorted"] == 5, (s0, s1)
+
+
+def test_unrecorded_arena_calls_between_records(gpu):
+    """Between two calls that record their extent (one in kAutoRefresh), the arena path runs without the
+    extent kernel and without the device check: the declared range is checked on the host to lie in one
+    allocation and payloads outside it are folded directly. Twenty calls, the layout rewritten in place
+    three times inside such windows, every digest exact."""
+    import torch
+
+    import annety_amd
+
+    data, offs, lens = _packed(6, 3000)
+    data = np.concatenate([data, np.zeros(70000, dtype=np.uint8)])
+    d, o, ln = _dev(gpu, data, offs, lens)
+    out = torch.empty(len(lens), dtype=torch.int32, device=gpu)
+    s0 = annety_amd.var_path_stats(0)
+    layouts = {9: offs + 300, 13: offs[::-1].copy(), 17: offs.copy()}
+    layouts[17][len(offs) // 3:] += 9000  # a 9 KiB gap: the payloads after it leave the declared range
+    cur = offs
+    for i in range(20):
+        if i in layouts:
+            cur = layouts[i]
+            o.copy_(torch.from_numpy(cur))
+        out.fill_(7)
+        annety_amd.crc32_batch_var(d, o, ln, out=out)
+        _check(out, data, cur, lens)
+    s1 = annety_amd.var_path_stats(0)
+    assert s1["arena_unrecorded"] - s0["arena_unrecorded"] >= 10, (s0, s1)
