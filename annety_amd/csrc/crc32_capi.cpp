@@ -644,6 +644,15 @@ size_t sorted_scratch_bytes(size_t n) {
   return (rows_words + 8) * sizeof(uint32_t) + 16 * n;  // rows + ranges (16-byte multiple) + descriptors
 }
 
+// The length classes in one launch (1, default) or one launch each (ANNETY_CRC_SORTED_FUSED=0). Read once.
+bool sorted_fused() {
+  static const bool on = [] {
+    const char* e = std::getenv("ANNETY_CRC_SORTED_FUSED");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // The sorted path's launches into `slot` (sized by sorted_scratch_bytes; c.arena_mu held). `record`
 // (automatic path): the extent record the bucket pass publishes, numbered `seq`.
 int run_var_sorted_in(DeviceCtx& c, DeviceCtx::ScratchSlot* slot, const void* d_base, size_t n, const uint64_t* d_off,
@@ -675,6 +684,21 @@ int run_var_sorted_in(DeviceCtx& c, DeviceCtx::ScratchSlot* slot, const void* d_
   }
   slot->sorts++;
   int rc = ANNETY_CRC_OK;
+  if (sorted_fused()) {  // the three length classes in one launch (crc32_var_sorted_kernel)
+    VarLaunch a{};
+    a.update = update;
+    a.base = d_base;
+    a.n = n;
+    a.desc = bk.desc;
+    a.range = bk.ranges;
+    a.img_slice = c.d_slice;
+    a.img_unshift = c.d_unshift;
+    a.short_init = c.d_short;
+    a.out = d_out;
+    a.max_blocks = grid_cus(c);
+    const hipError_t e = launch_var_sorted(a, group_image(c, 32), group_image(c, 16), group_image(c, 4), stream);
+    return e == hipSuccess ? ANNETY_CRC_OK : hip_fail(e);
+  }
   const uint32_t groups[3] = {32, 16, 4};  // lanes per payload of the long / middle / small class
   for (int k = 0; k < 3 && rc == ANNETY_CRC_OK; k++)
     rc = run_var(c, d_base, n, 0, 0, groups[k], bk.desc, bk.ranges + 2 * k, d_out, stream, update);

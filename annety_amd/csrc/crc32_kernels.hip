@@ -266,17 +266,15 @@ __device__ __forceinline__ uint4 raw_task(size_t t, size_t end, const uint8_t* b
 //        shift_len(s) ^ raw(M, 0) below that.
 //   PROBE (microbench only; product = 0): bit 0 drops the byte masks, bit 1 the unshift - wrong
 //        digests, used to measure what those stages cost (microbench/ab3.hip).
-template <int G, bool SORTED, bool UPD = false, int VWG = kVwg, int PROBE = 0>
-__global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __restrict__ base, size_t n,
-                                                           uint64_t fstride, uint32_t flen,
-                                                           const uint4* __restrict__ desc,
-                                                           const uint32_t* __restrict__ range,
-                                                           const uint4* __restrict__ img_slice,
-                                                           const uint4* __restrict__ img_group,
-                                                           const uint4* __restrict__ img_unshift,
-                                                           const uint32_t* __restrict__ short_init,
-                                                           uint32_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsVarImageBytes / 16];
+//   STAGE: which parts of the LDS image this call stages - 2 = all of it, and none when the block has no
+//        task (a kernel of its own); 1 = all of it always; 0 = only the G-specific group part (the later
+//        length classes of crc32_var_sorted_kernel, whose first class staged the rest).
+template <int G, bool SORTED, bool UPD, int VWG, int PROBE, int STAGE>
+__device__ __forceinline__ void var_class(uint4* lds4, const uint8_t* __restrict__ base, size_t n, uint64_t fstride,
+                                          uint32_t flen, const uint4* __restrict__ desc,
+                                          const uint32_t* __restrict__ range, const uint4* __restrict__ img_slice,
+                                          const uint4* __restrict__ img_group, const uint4* __restrict__ img_unshift,
+                                          uint32_t* __restrict__ out) {
   const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
 
   const uint32_t j = threadIdx.x & (G - 1);
@@ -309,7 +307,13 @@ __global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __rest
   size_t t0 = t_begin + gid;
   // a block with no task (an empty length class of the sorted path, or fewer tasks than lane groups)
   // leaves before its first descriptor load and the image staging
-  if (!__syncthreads_or(t0 < t_end)) return;
+  if (!__syncthreads_or(t0 < t_end)) {
+    if constexpr (STAGE == 1) {
+      load_image<kLdsVarImageBytes>(lds4, img_slice, img_group, img_unshift);
+      __syncthreads();
+    }
+    return;
+  }
   VarTask dec0 = decode_task<G>(raw(t0), t0 < t_end);
   if constexpr (UPD) dec0.state = dec0.valid ? out[dec0.p] : 0u;
   uint32_t r0 = 0;
@@ -319,7 +323,10 @@ __global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __rest
 
   uint4 A[8], B[8];
   load(dec0, r0, A);
-  load_image<kLdsVarImageBytes>(lds4, img_slice, img_group, img_unshift);
+  if constexpr (STAGE == 0)
+    load_image<kLdsImageBytes, kBlock, kLdsImageBytes, kLdsCommonBytes>(lds4, img_slice, img_group);
+  else
+    load_image<kLdsVarImageBytes>(lds4, img_slice, img_group, img_unshift);
   __syncthreads();
 
   uint32_t s = 0;
@@ -429,6 +436,44 @@ __global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __rest
     step(A, B);
     step(B, A);  // harmless when the group ran out of work on the first half: nothing is stored
   }
+}
+
+template <int G, bool SORTED, bool UPD = false, int VWG = kVwg, int PROBE = 0>
+__global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __restrict__ base, size_t n,
+                                                           uint64_t fstride, uint32_t flen,
+                                                           const uint4* __restrict__ desc,
+                                                           const uint32_t* __restrict__ range,
+                                                           const uint4* __restrict__ img_slice,
+                                                           const uint4* __restrict__ img_group,
+                                                           const uint4* __restrict__ img_unshift,
+                                                           const uint32_t* __restrict__ short_init,
+                                                           uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsVarImageBytes / 16];
+  var_class<G, SORTED, UPD, VWG, PROBE, 2>(lds4, base, n, fstride, flen, desc, range, img_slice, img_group,
+                                           img_unshift, out);
+}
+
+// The sorted path's three length classes in one launch (ranges[0..5] = the classes' [begin, end) in desc,
+// longest first): each block runs its share of the G = 32 class, then of the G = 16 class (restaging only
+// the group part of the image), then of the G = 4 class. A block that finishes a class early starts the
+// next one instead of waiting for the class's slowest lane groups (three launches drained each class:
+// a 64 KiB-payload launch loses ~24 us to its tail), and two launch gaps go.
+template <bool UPD>
+__global__ __launch_bounds__(kBlock) void crc32_var_sorted_kernel(const uint8_t* __restrict__ base, size_t n,
+                                                                  const uint4* __restrict__ desc,
+                                                                  const uint32_t* __restrict__ ranges,
+                                                                  const uint4* __restrict__ img_slice,
+                                                                  const uint4* __restrict__ img_g32,
+                                                                  const uint4* __restrict__ img_g16,
+                                                                  const uint4* __restrict__ img_g4,
+                                                                  const uint4* __restrict__ img_unshift,
+                                                                  uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsVarImageBytes / 16];
+  var_class<32, true, UPD, kVwg, 0, 1>(lds4, base, n, 0, 0, desc, ranges, img_slice, img_g32, img_unshift, out);
+  __syncthreads();  // every wave is done with the G = 32 group tables
+  var_class<16, true, UPD, kVwg, 0, 0>(lds4, base, n, 0, 0, desc, ranges + 2, img_slice, img_g16, img_unshift, out);
+  __syncthreads();
+  var_class<4, true, UPD, kVwg, 0, 0>(lds4, base, n, 0, 0, desc, ranges + 4, img_slice, img_g4, img_unshift, out);
 }
 
 // ---- long payloads: segments + CRC combine ----
@@ -574,6 +619,21 @@ hipError_t launch_fixed(const FixedLaunch& a, hipStream_t stream) {
   if (!a.raw && a.full && a.rounds == 1) return launch_one(a, stream);
   if (a.raw) return a.full ? launch_full<true, true>(a, stream) : launch_full<false, true>(a, stream);
   return a.full ? launch_full<true, false>(a, stream) : launch_full<false, false>(a, stream);
+}
+
+hipError_t launch_var_sorted(const VarLaunch& a, const void* img_g32, const void* img_g16, const void* img_g4,
+                             hipStream_t stream) {
+  const unsigned blocks = (unsigned)std::max<size_t>(1, a.max_blocks);
+#define ANNETY_SORTED_LAUNCH(UPD)                                                                             \
+  hipLaunchKernelGGL((crc32_var_sorted_kernel<UPD>), dim3(blocks), dim3(kBlock), 0, stream,                  \
+                     static_cast<const uint8_t*>(a.base), a.n, static_cast<const uint4*>(a.desc), a.range,      \
+                     static_cast<const uint4*>(a.img_slice), static_cast<const uint4*>(img_g32),               \
+                     static_cast<const uint4*>(img_g16), static_cast<const uint4*>(img_g4),                    \
+                     static_cast<const uint4*>(a.img_unshift), a.out)
+  if (a.update) ANNETY_SORTED_LAUNCH(true);
+  else ANNETY_SORTED_LAUNCH(false);
+#undef ANNETY_SORTED_LAUNCH
+  return hipGetLastError();
 }
 
 hipError_t launch_var(const VarLaunch& a, hipStream_t stream) {
