@@ -1,9 +1,9 @@
 // Arena path for variable-length batches whose payloads lie in one buffer (a NetBuffer, a frame
 // stream, a packed batch: BASELINE config 3). Two launches, no sort:
 //
-//  1. The line pass (crc32_oneround_kernel<8> in ARENA mode, crc32_kernels.hip) streams EVERY 128-byte
-//     line of the arena, payload-agnostic, in the access shape of the config-1 kernel (a wave reads 64
-//     consecutive lines = one 8 KiB superblock per round). Per line j of a 1 KiB block it stores the
+//  1. The line pass (crc32_arena_lines_kernel, crc32_arena_lines.h) streams EVERY 128-byte line of the
+//     arena, payload-agnostic, in the access shape of the config-1 kernel (a wave reads 64 consecutive
+//     lines = one 8 KiB superblock per round). Per line j of a 1 KiB block it stores the
 //     block-suffix CRC S[j] = raw(lines j..7) (register 0, no init), per block g of a superblock the
 //     superblock-suffix SB[g] = raw(blocks g..7). No payload state: the arena runs at the fixed-batch
 //     rate whatever the length mix.
