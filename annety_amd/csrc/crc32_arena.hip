@@ -284,7 +284,7 @@ struct Stitcher {
   }
 
   // Phase B: the S/SB words of the plan.
-  __device__ __forceinline__ void plan_b(size_t p, const Plan& y, Vals& v) const {
+  __device__ __forceinline__ void plan_b(size_t /*p*/, const Plan& y, Vals& v) const {
     const uint32_t dummy = 0;  // g.W0[0]: a valid word (the loads of inactive steps are not used)
 #pragma unroll
     for (int q = 0; q < 4; q++) {

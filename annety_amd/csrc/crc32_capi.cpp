@@ -211,7 +211,6 @@ struct HostImages {
   std::vector<uint32_t> unshift; // 24 maps x 128 words (U_lo[0..15], U_hi[0..7])
   std::vector<uint32_t> sb;      // arena superblock join: (k, v, g) = shift_{(7-g)*1024}(v << 4k)
   std::vector<uint32_t> stitch;  // arena stitch: segment maps F/G/UL/UB, unshift, shift_32 (crc32_math.h)
-  uint32_t short_init[4];
 };
 
 // Apply matrix m to (v << 4k) for every nibble value: the 16-entry table of one nibble position.
@@ -292,7 +291,6 @@ const HostImages& host_images() {
       nibble_tables(acc, img.unshift.data() + (16 + h) * 128);
       acc = gf2_mul(inv16, acc);
     }
-    for (int l = 0; l < 4; l++) img.short_init[l] = shift_bits(kInit, 8u * l);
     img.sb.assign(kLdsSbJoinBytes / 4, 0);
     for (uint32_t g = 0; g < 8; g++) {
       uint32_t nt[8 * 16];
@@ -357,7 +355,6 @@ struct DeviceCtx {
   void* d_slice = nullptr;
   void* d_groups = nullptr;
   uint32_t* d_unshift = nullptr;
-  uint32_t* d_short = nullptr;
   void* d_sb = nullptr;
   void* d_stitch = nullptr;
   void* d_zero = nullptr;  // 256 zero bytes
@@ -413,11 +410,11 @@ size_t grid_cus(const DeviceCtx& c) { return (size_t)std::max(1, c.cus - g_reser
 std::mutex g_init_mu;
 
 void free_images(DeviceCtx& c) {
-  void* bufs[] = {c.d_slice, c.d_groups, c.d_unshift, c.d_short, c.d_sb, c.d_stitch, c.d_zero};
+  void* bufs[] = {c.d_slice, c.d_groups, c.d_unshift, c.d_sb, c.d_stitch, c.d_zero};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   c.d_slice = c.d_groups = nullptr;
-  c.d_unshift = c.d_short = nullptr;
+  c.d_unshift = nullptr;
   c.d_sb = c.d_stitch = c.d_zero = nullptr;
 }
 
@@ -440,7 +437,6 @@ int init_device_locked(int dev) {
     if ((e = hipMalloc(&c.d_slice, img.slice.size() * 4)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMalloc(&c.d_groups, img.groups.size() * 4)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMalloc(&c.d_unshift, img.unshift.size() * 4)) != hipSuccess) { rc = hip_fail(e); break; }
-    if ((e = hipMalloc(&c.d_short, 16)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMalloc(&c.d_sb, img.sb.size() * 4)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMalloc(&c.d_stitch, img.stitch.size() * 4)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMalloc(&c.d_zero, 256)) != hipSuccess) { rc = hip_fail(e); break; }
@@ -450,7 +446,6 @@ int init_device_locked(int dev) {
     if ((e = hipMemcpy(c.d_slice, img.slice.data(), img.slice.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMemcpy(c.d_groups, img.groups.data(), img.groups.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMemcpy(c.d_unshift, img.unshift.data(), img.unshift.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_fail(e); break; }
-    if ((e = hipMemcpy(c.d_short, img.short_init, 16, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_fail(e); break; }
     c.cus = prop.multiProcessorCount;
     c.ready = true;
   } while (0);
@@ -556,7 +551,6 @@ int run_var(DeviceCtx& c, const void* d_base, size_t n, uint64_t fstride, uint32
   a.img_slice = c.d_slice;
   a.img_group = group_image(c, group);
   a.img_unshift = c.d_unshift;
-  a.short_init = c.d_short;
   a.out = d_out;
   a.max_blocks = grid_cus(c);
   HIP_TRY(launch_var(a, stream));
@@ -693,7 +687,6 @@ int run_var_sorted_in(DeviceCtx& c, DeviceCtx::ScratchSlot* slot, const void* d_
     a.range = bk.ranges;
     a.img_slice = c.d_slice;
     a.img_unshift = c.d_unshift;
-    a.short_init = c.d_short;
     a.out = d_out;
     a.max_blocks = grid_cus(c);
     const hipError_t e = launch_var_sorted(a, group_image(c, 32), group_image(c, 16), group_image(c, 4), stream);

@@ -41,7 +41,6 @@ struct VarLaunch {
   const void* img_slice;
   const void* img_group;
   const void* img_unshift;   // 12 KiB two-level inverse-shift tables (LDS image part 3)
-  const uint32_t* short_init;  // shift_len(0xFFFFFFFF) for len = 0..3
   uint32_t* out;             // digests, or (update) the register array, read and written in place
   size_t max_blocks;
   bool update;               // crc32_update semantics instead of crc32_long

@@ -21,14 +21,14 @@
 namespace annety_crc {
 namespace {
 
-// Fixed-length batch: payload p = base + p*stride, `len_blocks` 16-byte blocks, 16-byte aligned.
+// Fixed-length batch: payload p = base + p*stride, 16-byte aligned, `rounds` rounds of G lines per payload.
 // Chunks are aligned to the payload END (virtual leading zero blocks pad the first round), so every
 // lane's last chunk ends (G-1-j)*128 bytes before the payload end and the join maps are constants.
 //   FULL  : len is a multiple of G*128 (no virtual blocks)
 //   RAW   : crc32_update semantics - no init injection, no final xor; state_in folded in by the writer
 template <int G, bool FULL, bool RAW, int VWG = kVwg>
 __global__ __launch_bounds__(kBlock) void crc32_fixed_kernel(const uint8_t* __restrict__ base, size_t n,
-                                                             uint32_t len_blocks, size_t stride, uint32_t rounds,
+                                                             size_t stride, uint32_t rounds,
                                                              uint32_t vlead, const uint4* __restrict__ img_slice,
                                                              const uint4* __restrict__ img_group,
                                                              const ShiftCols raw_shift_cols,
@@ -446,7 +446,6 @@ __global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __rest
                                                            const uint4* __restrict__ img_slice,
                                                            const uint4* __restrict__ img_group,
                                                            const uint4* __restrict__ img_unshift,
-                                                           const uint32_t* __restrict__ short_init,
                                                            uint32_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsVarImageBytes / 16];
   var_class<G, SORTED, UPD, VWG, PROBE, 2>(lds4, base, n, fstride, flen, desc, range, img_slice, img_group,
@@ -551,7 +550,7 @@ hipError_t launch_var_g(const VarLaunch& a, hipStream_t stream) {
                      static_cast<const uint8_t*>(a.base), a.n, a.fixed_stride, a.fixed_len,                  \
                      static_cast<const uint4*>(a.desc), a.range, static_cast<const uint4*>(a.img_slice),     \
                      static_cast<const uint4*>(a.img_group), static_cast<const uint4*>(a.img_unshift),       \
-                     a.short_init, a.out)
+                     a.out)
   if (a.desc) {
     if (a.update) ANNETY_VAR_LAUNCH(true, true);
     else ANNETY_VAR_LAUNCH(true, false);
@@ -570,7 +569,7 @@ hipError_t launch_g(const FixedLaunch& a, hipStream_t stream) {
   if (blocks > a.max_blocks) blocks = a.max_blocks;
   if (blocks == 0) return hipSuccess;
   hipLaunchKernelGGL((crc32_fixed_kernel<G, FULL, RAW>), dim3((unsigned)blocks), dim3(kBlock), 0, stream,
-                     static_cast<const uint8_t*>(a.base), a.n, a.len_blocks, a.stride, a.rounds, a.vlead,
+                     static_cast<const uint8_t*>(a.base), a.n, a.stride, a.rounds, a.vlead,
                      static_cast<const uint4*>(a.img_slice), static_cast<const uint4*>(a.img_group), a.raw_shift_cols,
                      a.out);
   return hipGetLastError();

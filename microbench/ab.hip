@@ -59,14 +59,14 @@ __global__ __launch_bounds__(kBlock) void var_kernel(const uint8_t* __restrict__
       for (int i = 0; i < 8; i++) B[i] = s[i];
     }
     __builtin_amdgcn_sched_barrier(0);
-    finish(absorb_line(sinit, A, k));
+    finish(absorb_line(sinit, A, k, lds));
     if (t + 2 < ntasks) {
       const uint4* s = reinterpret_cast<const uint4*>(lp + 2 * pstep);
 #pragma unroll
       for (int i = 0; i < 8; i++) A[i] = s[i];
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (t + 1 < ntasks) finish(absorb_line(sinit, B, k));
+    if (t + 1 < ntasks) finish(absorb_line(sinit, B, k, lds));
     lp += 2 * pstep;
   }
 }

@@ -26,8 +26,7 @@ void launch_probe(DeviceCtx& c, const void* d, size_t n, uint32_t L, uint32_t* o
   const size_t blocks = std::min<size_t>(256, (n * G + kBlock - 1) / kBlock);
   hipLaunchKernelGGL((crc32_var_kernel<G, false, false, kVwg, PROBE>), dim3((unsigned)blocks), dim3(kBlock), 0, 0,
                      (const uint8_t*)d, n, (uint64_t)L, L, (const uint4*)nullptr, (const uint32_t*)nullptr,
-                     (const uint4*)c.d_slice, (const uint4*)group_image(c, G), (const uint4*)c.d_unshift, c.d_short,
-                     out);
+                     (const uint4*)c.d_slice, (const uint4*)group_image(c, G), (const uint4*)c.d_unshift, out);
 }
 
 int main() {

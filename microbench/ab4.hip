@@ -29,7 +29,7 @@ template <int G, int PROBE>
 void launch_cls(DeviceCtx& c, const void* base, size_t n, const void* desc, const uint32_t* range, uint32_t* out) {
   hipLaunchKernelGGL((crc32_var_kernel<G, true, false, kVwg, PROBE>), dim3(c.cus), dim3(kBlock), 0, 0,
                      (const uint8_t*)base, n, (uint64_t)0, 0u, (const uint4*)desc, range, (const uint4*)c.d_slice,
-                     (const uint4*)group_image(c, G), (const uint4*)c.d_unshift, c.d_short, out);
+                     (const uint4*)group_image(c, G), (const uint4*)c.d_unshift, out);
 }
 
 int main() {
