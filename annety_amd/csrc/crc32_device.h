@@ -218,6 +218,65 @@ __device__ __forceinline__ uint4 gload16(uint64_t addr) {
 #define ANNETY_PRIO_HI() do { if constexpr (ANNETY_PRIO) __builtin_amdgcn_s_setprio(ANNETY_PRIO); } while (0)
 #define ANNETY_PRIO_LO() do { if constexpr (ANNETY_PRIO) __builtin_amdgcn_s_setprio(0); } while (0)
 
+// Coalesced loads for a wave's 8 KiB (64 consecutive 128-byte lines, line m = 8 b + j: block b, line j):
+// load i covers block i whole, 16 B per lane, lane l reading chunk 4 l3 + 2 l5 + l4 of line j = l & 7 (lk =
+// bit k of l). Every load is a contiguous 1 KiB, so it can be nontemporal (per-line loads, which touch 64 lines
+// per instruction, run 2.4x slower nontemporal). coalesced_lane_offset() is that lane's byte offset inside a
+// block. transpose_blocks() then swaps register bit 0 with lane bit 4 (permlane16) and register bit 1 with lane
+// bit 5 (permlane32), one swap per dword pair: lane l holds half l3 of line j of block 2 l5 + l4 in v[0..3] and
+// of block 4 + 2 l5 + l4 in v[4..7], ready for fold_halves(). DESIGN.md §2.3.
+__device__ __forceinline__ uint32_t coalesced_lane_offset(uint32_t l) {
+  return 128u * (l & 7u) + 16u * (4u * ((l >> 3) & 1u) + 2u * ((l >> 5) & 1u) + ((l >> 4) & 1u));
+}
+template <int D>
+__device__ __forceinline__ void swap_stage(uint4 (&v)[8]) {
+#pragma unroll
+  for (int r = 0; r < 8; r++) {
+    if (r & D) continue;
+    uint32_t* a = reinterpret_cast<uint32_t*>(&v[r]);
+    uint32_t* b = reinterpret_cast<uint32_t*>(&v[r | D]);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      if constexpr (D == 1) {
+        const auto p = __builtin_amdgcn_permlane16_swap(a[q], b[q], false, false);
+        a[q] = p[0];
+        b[q] = p[1];
+      } else {
+        const auto p = __builtin_amdgcn_permlane32_swap(a[q], b[q], false, false);
+        a[q] = p[0];
+        b[q] = p[1];
+      }
+    }
+  }
+}
+__device__ __forceinline__ void transpose_blocks(uint4 (&v)[8]) {
+  swap_stage<1>(v);
+  swap_stage<2>(v);
+}
+// After transpose_blocks: the raw CRC (register 0) of line l & 7 of block 4 l3 + 2 l5 + l4. The two 64-byte
+// chains v[0..3] and v[4..7] are half l3 of two lines; the halves meet across lane bit 3 (DPP row_ror:8 =
+// lane ^ 8): lanes with l3 = 0 keep their first block's line, lanes with l3 = 1 their second block's,
+// raw(line) = shift_64(raw(first half)) ^ raw(second half).
+__device__ __forceinline__ uint32_t fold_halves(const uint4 (&v)[8], const LaneCtx& k, const uint32_t* lds,
+                                                uint32_t l3) {
+  uint32_t xa = v[0].x, xb = v[4].x;
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    word4x2(xa, v[i].y, xb, v[4 + i].y, k);
+    word4x2(xa, v[i].z, xb, v[4 + i].z, k);
+    word4x2(xa, v[i].w, xb, v[4 + i].w, k);
+    word4x2(xa, i + 1 < 4 ? v[i + 1].x : 0u, xb, i + 1 < 4 ? v[5 + i].x : 0u, k);
+  }
+  const uint32_t send = l3 ? xa : xb;
+  const uint32_t got = (uint32_t)__builtin_amdgcn_mov_dpp((int)send, 0x128, 0xF, 0xF, false);
+  const uint32_t first = l3 ? got : xa, second = l3 ? xb : got;
+  return nibble_map_uniform(first, lds, kLdsHalfOff) ^ second;
+}
+// Block of a lane's line after fold_halves.
+__device__ __forceinline__ uint32_t folded_block(uint32_t l) {
+  return 4u * ((l >> 3) & 1u) + 2u * ((l >> 5) & 1u) + ((l >> 4) & 1u);
+}
+
 // Keep bytes [lo8/8, hi8/8) of a line (N = 8) or half line (N = 4), zero the rest (branch-free, per
 // 32-bit word).
 template <int N>

@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdlib>
 
 #include "crc32_device.h"
 #include "crc32_kernels.h"
@@ -203,6 +204,70 @@ __global__ __launch_bounds__(BLK) void crc32_oneround_kernel(const uint8_t* __re
     ANNETY_PRIO_LO();
     if (t + 1 < ntasks) finish(absorb_line(sinit, B, k, lds));
     lp += 2 * pstep;
+  }
+}
+
+// Contiguous 1 KiB payloads (stride 1024, n a multiple of 8: BASELINE configs 1 and 4): the one-round
+// kernel's work with coalesced nontemporal loads. A wave's task is 8 consecutive payloads (8 KiB); load i reads
+// payload i whole (1 KiB contiguous, 16 B per lane) and transpose_blocks() / fold_halves() (crc32_device.h)
+// bring each lane one line, of payload folded_block(lane). Same box, alternating: 167-169 us per 1 GiB launch
+// against 180 us for crc32_oneround_kernel<8> (microbench/nt_mb.hip). Addresses are one scalar base per task
+// plus immediate offsets: with a runtime stride the per-load scalar arithmetic cost 7 us of it.
+template <int BLK = kBlock, int VWG = kVwg>
+__global__ __launch_bounds__(BLK) void crc32_onekib_nt_kernel(const uint8_t* __restrict__ base, size_t n,
+                                                              const uint4* __restrict__ img_slice,
+                                                              const uint4* __restrict__ img_group,
+                                                              uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsImageBytes / 16];
+  const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
+  const uint32_t l = threadIdx.x & 63, j = l & 7, l3 = (l >> 3) & 1;
+  const size_t gid = group_id<BLK, 8, VWG>();
+  // the wave's first payload (its 8 lane groups are 8 consecutive groups), wave-uniform
+  const size_t p0 = ((size_t)__builtin_amdgcn_readfirstlane((uint32_t)(gid >> 32)) << 32) |
+                    (size_t)(__builtin_amdgcn_readfirstlane((uint32_t)gid) & ~7u);
+  const size_t ngroups = ((size_t)gridDim.x * BLK) / 8;
+  const int ntasks = p0 < n ? (int)((n - 1 - p0) / ngroups + 1) : 0;
+  LaneCtx k;
+  k.L0 = (threadIdx.x & 31) << 3;
+  k.L1 = k.L0 | (1u << 16);
+  k.slot4 = (threadIdx.x & 31) << 2;
+  const uint32_t lane_off = coalesced_lane_offset(l);
+  const uint32_t sinit = (j == 0 && l3 == 0) ? kInit : 0u;  // the payloads' first words (line 0, half 0)
+  const uint8_t* wp = base + p0 * 1024 + lane_off;
+  const size_t pstep = ngroups * 1024;
+  uint32_t* op = out + p0 + folded_block(l);
+  auto load = [&](const uint8_t* a, uint4 (&v)[8]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const v4u32 x = __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(a + 1024 * i));
+      v[i] = make_uint4(x.x, x.y, x.z, x.w);
+    }
+  };
+  uint4 A[8], B[8];
+  if (ntasks > 0) load(wp, A);
+  load_image<kLdsImageBytes, BLK>(lds4, img_slice, img_group);
+  __syncthreads();
+  auto finish = [&](uint4 (&v)[8]) __attribute__((always_inline)) {
+    transpose_blocks(v);
+    v[0].x ^= sinit;
+    v[4].x ^= sinit;
+    const uint32_t c = group_xor_reduce<8>(nibble_map_lane(fold_halves(v, k, lds, l3), lds, k.slot4));
+    if (j == 7) *op = ~c;
+    op += ngroups;
+  };
+  // unconditional loads, as in crc32_oneround_kernel (past the last task a wave re-reads its current one)
+  for (int t = 0; t < ntasks; t += 2) {
+    ANNETY_PRIO_HI();
+    load(t + 1 < ntasks ? wp + pstep : wp, B);
+    __builtin_amdgcn_sched_barrier(0);
+    ANNETY_PRIO_LO();
+    finish(A);
+    ANNETY_PRIO_HI();
+    load(t + 2 < ntasks ? wp + 2 * pstep : wp, A);
+    __builtin_amdgcn_sched_barrier(0);
+    ANNETY_PRIO_LO();
+    if (t + 1 < ntasks) finish(B);
+    wp += 2 * pstep;
   }
 }
 
@@ -587,7 +652,25 @@ hipError_t launch_one_g(const FixedLaunch& a, hipStream_t stream) {
   return hipGetLastError();
 }
 
+// ANNETY_CRC_FIXED_NT=0 keeps contiguous 1 KiB batches on crc32_oneround_kernel<8> (A/B), read once.
+bool onekib_nt_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("ANNETY_CRC_FIXED_NT");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 hipError_t launch_one(const FixedLaunch& a, hipStream_t stream) {
+  if (a.group == 8 && a.stride == 1024 && a.n % 8 == 0 && onekib_nt_enabled()) {
+    size_t blocks = (a.n * 8 + kBlock - 1) / kBlock;
+    if (blocks > a.max_blocks) blocks = a.max_blocks;
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL((crc32_onekib_nt_kernel<>), dim3((unsigned)blocks), dim3(kBlock), 0, stream,
+                       static_cast<const uint8_t*>(a.base), a.n, static_cast<const uint4*>(a.img_slice),
+                       static_cast<const uint4*>(a.img_group), a.out);
+    return hipGetLastError();
+  }
   switch (a.group) {
     case 1: return launch_one_g<1>(a, stream);
     case 2: return launch_one_g<2>(a, stream);

@@ -21,7 +21,25 @@ using namespace annety_crc;
 
 namespace {
 
-template <int MAP, int EXTRA>
+// One 128-byte line as four 32-byte chains (16 LDS reads per wait instead of 8): timing only, the joins
+// use the half-line map for every chain (the arena image has no shift_32 / shift_96 tables).
+__device__ __forceinline__ uint32_t absorb_line4(const uint4 (&v)[8], const LaneCtx& k, const uint32_t* lds) {
+  uint32_t xa = v[0].x, xb = v[2].x, xc = v[4].x, xd = v[6].x;
+#pragma unroll
+  for (int i = 0; i < 2; i++) {
+    word4x4(xa, v[i].y, xb, v[2 + i].y, xc, v[4 + i].y, xd, v[6 + i].y, k);
+    word4x4(xa, v[i].z, xb, v[2 + i].z, xc, v[4 + i].z, xd, v[6 + i].z, k);
+    word4x4(xa, v[i].w, xb, v[2 + i].w, xc, v[4 + i].w, xd, v[6 + i].w, k);
+    word4x4(xa, i == 0 ? v[1].x : 0u, xb, i == 0 ? v[3].x : 0u, xc, i == 0 ? v[5].x : 0u, xd, i == 0 ? v[7].x : 0u, k);
+  }
+  return nibble_map_uniform(xa, lds, kLdsHalfOff) ^ nibble_map_uniform(xb, lds, kLdsHalfOff) ^
+         nibble_map_uniform(xc, lds, kLdsHalfOff) ^ xd;
+}
+
+// LM (load mode): 0 = a lane reads its own 128-byte line as 8 x 16 B (the product); 1 = coalesced, load i
+// of a wave covers bytes [1024 i, 1024 i + 1024) of its 8 KiB (16 B per lane); 2 = 1 with nontemporal loads.
+// Modes 1 and 2 fold the bytes in the wrong order (timing only).
+template <int MAP, int EXTRA, int LM = 0>
 __global__ __launch_bounds__(kBlock) void k_region(const uint8_t* __restrict__ base, uint64_t nsb,
                                                    const uint4* __restrict__ img_slice,
                                                    const uint4* __restrict__ img_group8,
@@ -75,18 +93,32 @@ __global__ __launch_bounds__(kBlock) void k_region(const uint8_t* __restrict__ b
   k.L0 = (threadIdx.x & 31) << 3;
   k.L1 = k.L0 | (1u << 16);
   k.slot4 = (threadIdx.x & 31) << 2;
-  const uint8_t* lp = base + s * 8192 + g * 1024 + j * 128;
-  uint4 A[8], B[8];
-  if (ntasks > 0) {
+  const uint8_t* lp = base + s * 8192 + (LM == 0 ? g * 1024 + j * 128 : lane * 16);
+  constexpr uint32_t ES = LM == 0 ? 16 : 1024;
+  auto ld = [&](const uint8_t* q, uint4 (&v)[8]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < 8; i++) A[i] = reinterpret_cast<const uint4*>(lp)[i];
-  }
+    for (int i = 0; i < 8; i++) {
+      const uint4* a = reinterpret_cast<const uint4*>(q + i * ES);
+      if constexpr (LM == 2) {
+        const v4u32 x = __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(a));
+        v[i] = make_uint4(x.x, x.y, x.z, x.w);
+      } else {
+        v[i] = *a;
+      }
+    }
+  };
+  uint4 A[8], B[8];
+  if (ntasks > 0) ld(lp, A);
   load_image<kLdsArenaImageBytes, kBlock>(lds4, img_slice, img_group8, img_sb);
   __syncthreads();
   uint32_t acc = 0;
   auto finish = [&](const uint4 (&v)[8], int t) __attribute__((always_inline)) {
-    const uint32_t r = absorb_line(0u, v, k, lds);
-    if constexpr (EXTRA == 0) {
+    uint32_t r;
+    if constexpr (EXTRA == 4)
+      r = absorb_line4(v, k, lds);
+    else
+      r = absorb_line(0u, v, k, lds);
+    if constexpr (EXTRA == 0 || EXTRA == 4) {
       acc ^= r;
     } else {
       uint32_t x = nibble_map_lane(r, lds, k.slot4);
@@ -141,9 +173,7 @@ __global__ __launch_bounds__(kBlock) void k_region(const uint8_t* __restrict__ b
     {
       const uint8_t* nx = lp + pstep;
       if constexpr (MAP == 3) nx = (uint64_t)(uintptr_t)nx >= wrap_at ? nx - wrap_to : nx;
-      const uint4* q = reinterpret_cast<const uint4*>(t + 1 < ntasks ? nx : lp);
-#pragma unroll
-      for (int i = 0; i < 8; i++) B[i] = q[i];
+      ld(t + 1 < ntasks ? nx : lp, B);
     }
     __builtin_amdgcn_sched_barrier(0);
     ANNETY_PRIO_LO();
@@ -155,9 +185,7 @@ __global__ __launch_bounds__(kBlock) void k_region(const uint8_t* __restrict__ b
         nx = (uint64_t)(uintptr_t)(lp + pstep) >= wrap_at ? nx - wrap_to : nx;
         nx = (uint64_t)(uintptr_t)nx >= wrap_at ? nx - wrap_to : nx;
       }
-      const uint4* q = reinterpret_cast<const uint4*>(t + 2 < ntasks ? nx : lp);
-#pragma unroll
-      for (int i = 0; i < 8; i++) A[i] = q[i];
+      ld(t + 2 < ntasks ? nx : lp, A);
     }
     __builtin_amdgcn_sched_barrier(0);
     ANNETY_PRIO_LO();
@@ -208,7 +236,16 @@ int main() {
     CK(hipEventElapsedTime(&ms, e0, e1));
     printf("%-44s %.1f us  %.0f GB/s\n", name, ms * 10, bytes / (ms / 100) / 1e6);
   };
+#define KL(M, X, L) [&] { hipLaunchKernelGGL((k_region<M, X, L>), dim3(256), dim3(kBlock), 0, 0, b, nsb, i0, i1, i2, out, dig); }
 #define K(M, X) [&] { hipLaunchKernelGGL((k_region<M, X>), dim3(256), dim3(kBlock), 0, 0, b, nsb, i0, i1, i2, out, dig); }
+  for (int rep = 0; rep < 3; rep++) {
+    t(K(0, 0), "map 0 grid-stride, fold only (2 chains)");
+    t(K(0, 4), "map 0 grid-stride, fold only (4 chains)");
+    t(KL(0, 0, 1), "map 0, fold only, coalesced loads");
+    t(KL(0, 0, 2), "map 0, fold only, coalesced nt loads");
+    t(KL(0, 0, 1), "map 0, fold only, coalesced loads");
+  }
+  if (getenv("ONLY_LOADS")) return 0;
   for (int rep = 0; rep < 2; rep++) {
     t([&] { CK(launch_arena_lines_p<0>(a, 0)); }, "product line pass (S + SB stores)");
     t([&] { CK(launch_arena_lines_p<3>(a, 0)); }, "product line pass PROBE 3 (no S, no SB)");
