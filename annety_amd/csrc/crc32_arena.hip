@@ -515,13 +515,13 @@ __global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(WPE))) void
 }
 
 // First launch: the line pass.
-template <int PROBE = 0>
+template <int PROBE = 0, bool NT = true>
 __global__ __launch_bounds__(kBlock) void crc32_arena_lines_kernel(const uint8_t* __restrict__ base, LineOut ar,
                                                                    const uint4* __restrict__ img_slice,
                                                                    const uint4* __restrict__ img_group8,
                                                                    const uint4* __restrict__ img_sb) {
   __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsArenaImageBytes / 16];
-  arena_line_pass<PROBE>(base, ar, blockIdx.x, gridDim.x, lds4, img_slice, img_group8, img_sb);
+  arena_line_pass<PROBE, NT>(base, ar, blockIdx.x, gridDim.x, lds4, img_slice, img_group8, img_sb);
 }
 
 // Extent of a variable batch (crc32_kernels.h launch_extent), no fences: every block writes its partial
@@ -793,17 +793,25 @@ hipError_t launch_stitch_lite(const ArenaLaunch& a, const void* img_lite, size_t
   return hipGetLastError();
 }
 
-template <int PROBE>
+template <int PROBE, bool NT = true>
 hipError_t launch_arena_lines_p(const ArenaLaunch& a, hipStream_t stream) {
   static_assert(kBlock / 8 == 64 && kSTasks == 8, "arena_geom / arena_s_word assume 64 groups per block, 8-task bursts");
   const ArenaGeom geo = arena_geom(a);
-  hipLaunchKernelGGL((crc32_arena_lines_kernel<PROBE>), dim3((unsigned)geo.blocks), dim3(kBlock), 0, stream,
+  hipLaunchKernelGGL((crc32_arena_lines_kernel<PROBE, NT>), dim3((unsigned)geo.blocks), dim3(kBlock), 0, stream,
                      reinterpret_cast<const uint8_t*>((uintptr_t)(a.fs0 * 8192)), line_out(a, geo), static_cast<const uint4*>(a.img_slice), static_cast<const uint4*>(a.img_group8),
                      static_cast<const uint4*>(a.img_sb));
   return hipGetLastError();
 }
 
-hipError_t launch_arena_lines(const ArenaLaunch& a, hipStream_t stream) { return launch_arena_lines_p<0>(a, stream); }
+// The line pass reads each superblock as 8 coalesced nontemporal 1 KiB loads (crc32_arena_lines.h);
+// ANNETY_CRC_LINES_NT=0 selects the per-line loads (A/B), read once.
+hipError_t launch_arena_lines(const ArenaLaunch& a, hipStream_t stream) {
+  static const bool nt = [] {
+    const char* e = std::getenv("ANNETY_CRC_LINES_NT");
+    return !(e && e[0] == '0');
+  }();
+  return nt ? launch_arena_lines_p<0, true>(a, stream) : launch_arena_lines_p<0, false>(a, stream);
+}
 
 hipError_t launch_arena(const ArenaLaunch& a, hipStream_t stream) {
   if (a.nsb) {

@@ -59,7 +59,11 @@ __device__ __forceinline__ bool extent_matches(const uint64_t* check, uint32_t p
 #ifndef ANNETY_S_NT
 #define ANNETY_S_NT 1
 #endif
-template <int PROBE = 0>
+// NT (product 1; 0 = the per-line loads, for A/B through ANNETY_CRC_LINES_NT=0): a wave's 8 KiB superblock
+// arrives as 8 coalesced nontemporal 1 KiB loads (one per block) and transpose_blocks() / fold_halves()
+// (crc32_device.h) leave lane l with line l & 7 of block folded_block(l); lane group q = l / 8 then holds block
+// bq = folded_block(8 q), and everything per block (the superblock join, SB, the S burst slots) follows bq.
+template <int PROBE = 0, bool NT = true>
 __device__ __forceinline__ void arena_line_pass(const uint8_t* __restrict__ base, const LineOut& ar, uint32_t bid,
                                                 uint32_t nbid, uint4* lds4,
                                                 const uint4* __restrict__ img_slice,
@@ -73,32 +77,49 @@ __device__ __forceinline__ void arena_line_pass(const uint8_t* __restrict__ base
   const size_t gid = (((size_t)bid + (size_t)nbid * (threadIdx.x / VWG)) * VWG + threadIdx.x % VWG) / 8;
   const size_t ngroups = (size_t)nbid * (BLK / 8);
   const size_t n = (size_t)(ar.fs1 - ar.fs0) * 8;  // full 1 KiB blocks = lane-group tasks
+  // n and ngroups are multiples of 8, so every lane of a wave has the same task count
   const int ntasks = gid < n ? (int)((n - 1 - gid) / ngroups + 1) : 0;
   const uint64_t pstep = ngroups * 1024;
+  const uint32_t lane = threadIdx.x & 63;
+  // this lane's block in its superblock, and the lane group holding block h
+  const uint32_t blk = NT ? folded_block(lane) : lane >> 3;
+  auto group_of = [](uint32_t h) { return NT ? (h >> 2) + 2 * (h & 1) + 4 * ((h >> 1) & 1) : h; };
+  // the wave's first lane group (wave-uniform: scalar addressing of the coalesced loads)
+  const size_t g0 = ((size_t)__builtin_amdgcn_readfirstlane((uint32_t)(gid >> 32)) << 32) |
+                    (size_t)(__builtin_amdgcn_readfirstlane((uint32_t)gid) & ~7u);
+  const size_t gblk = g0 + blk;  // the lane group whose block this lane's line is in
 
   LaneCtx k;
   k.L0 = (threadIdx.x & 31) << 3;
   k.L1 = k.L0 | (1u << 16);
   k.slot4 = (threadIdx.x & 31) << 2;
 
-  const uint8_t* lp = base + gid * 1024 + (size_t)j * kChunkBytes;
-  uint4 A[8], B[8];
-  if (ntasks > 0) {
+  const uint8_t* lp = NT ? base + g0 * 1024 + coalesced_lane_offset(lane) : base + gid * 1024 + (size_t)j * kChunkBytes;
+  auto load = [&](const uint8_t* a, uint4 (&v)[8]) __attribute__((always_inline)) {
 #pragma unroll
-    for (int i = 0; i < 8; i++) A[i] = reinterpret_cast<const uint4*>(lp)[i];
-  }
+    for (int i = 0; i < 8; i++) {
+      if constexpr (NT) {
+        const v4u32 x = __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(a + 1024 * i));
+        v[i] = make_uint4(x.x, x.y, x.z, x.w);
+      } else {
+        v[i] = reinterpret_cast<const uint4*>(a)[i];
+      }
+    }
+  };
+  uint4 A[8], B[8];
+  if (ntasks > 0) load(lp, A);
   load_image<kLdsArenaImageBytes, BLK>(lds4, img_slice, img_group8, img_sb);
   __syncthreads();
 
-  const uint32_t lane = threadIdx.x & 63;
   // S of 8 consecutive tasks leaves in two 16-byte stores per lane, each 1 KiB contiguous per wave:
   // interleaved with the read stream, a dword per lane per task cost 30 us of a 211 us pass, 16-byte
   // quads of 4 tasks 20 (microbench/arena_mb.hip).
   uint32_t q[kSTasks];
 #pragma unroll
   for (uint32_t i = 0; i < kSTasks; i++) q[i] = 0;
-  // r = raw CRC of this lane's line; returns S for it and (lanes j == 0) SB for its block
-  auto arena_scan = [&](uint32_t r, uint32_t& sbv) {
+  // r = raw CRC of this lane's line (line j of block b, its lane group holding the block's 8 lines in
+  // order; block h on lane group gq(h)); returns S for it and (lanes j == 0) SB for its block
+  auto arena_scan = [&](uint32_t r, uint32_t& sbv, uint32_t b, auto gq) {
     uint32_t x = nibble_map_lane(r, lds, k.slot4);  // shift_{(7-j)*128}(r): the line seen from the block end
     // suffix scan over the 8 lanes of the group (DPP row_shl:d = the value of lane + d in its row of 16)
     uint32_t y;
@@ -110,22 +131,22 @@ __device__ __forceinline__ void arena_line_pass(const uint8_t* __restrict__ base
     x ^= j + 4 < 8 ? y : 0u;  // S: lines j..7
     sbv = 0;
     if constexpr ((PROBE & 2) == 0) {
-      // the 8 groups of a wave are one superblock, in order (g = lane / 8): block g seen from the
-      // superblock end on lane 8g, then the suffix scan of those 8 values in scalar registers
-      const uint32_t g = lane >> 3;
+      // the 8 blocks of a wave are one superblock: block b seen from the superblock end on its group's
+      // lane 0, then the suffix scan of those 8 values in scalar registers
       uint32_t u = 0;
-      if (j == 0) u = sb_join(x, lds, g);
+      if (j == 0) u = sb_join(x, lds, b);
       uint32_t t[8];
-      t[7] = (uint32_t)__builtin_amdgcn_readlane((int)u, 56);
+      t[7] = (uint32_t)__builtin_amdgcn_readlane((int)u, 8 * gq(7));
 #pragma unroll
-      for (int h = 6; h >= 0; h--) t[h] = t[h + 1] ^ (uint32_t)__builtin_amdgcn_readlane((int)u, 8 * h);
+      for (int h = 6; h >= 0; h--) t[h] = t[h + 1] ^ (uint32_t)__builtin_amdgcn_readlane((int)u, 8 * gq(h));
       sbv = t[0];
 #pragma unroll
-      for (uint32_t h = 1; h < 8; h++) sbv = g == h ? t[h] : sbv;  // SB: blocks g..7
+      for (uint32_t h = 1; h < 8; h++) sbv = b == h ? t[h] : sbv;  // SB: blocks b..7
     }
     return x;
   };
-  // partial superblocks at the arena ends (wave-uniform, two waves of the grid)
+  // partial superblocks at the arena ends (wave-uniform, two waves of the grid): per-line loads, line =
+  // lane, block = lane / 8
   const uint64_t gw = (uint64_t)bid * (BLK / 64) + (threadIdx.x >> 6);
   if (gw < 2) {
     const uint64_t sb = gw == 0 ? ar.sb0 : ar.sb0 + ar.nsb - 1;
@@ -140,26 +161,33 @@ __device__ __forceinline__ void arena_line_pass(const uint8_t* __restrict__ base
       const int32_t hi8 = line == ar.line_hi ? (int32_t)(((ar.byte_hi - 1) & 127) + 1) * 8 : 1024;
       mask_line(v, lo8, hi8);
       uint32_t sbv;
-      const uint32_t x = arena_scan(absorb_line(0u, v, k, lds), sbv);
+      const uint32_t x = arena_scan(absorb_line(0u, v, k, lds), sbv, lane >> 3, [](uint32_t h) { return h; });
       if constexpr ((PROBE & 1) == 0) ar.S_edge[gw * 64 + lane] = x;
       if (j == 0) ar.SB_edge[gw * 8 + (lane >> 3)] = sbv;
     }
   }
 
-  auto finish = [&](uint32_t s, int t) {
+  auto finish = [&](uint4 (&v)[8], int t) __attribute__((always_inline)) {
+    uint32_t r;
+    if constexpr (NT) {
+      transpose_blocks(v);
+      r = fold_halves(v, k, lds, (lane >> 3) & 1);
+    } else {
+      r = absorb_line(0u, v, k, lds);
+    }
     uint32_t sbv;
-    const uint32_t x = arena_scan(s, sbv);
+    const uint32_t x = arena_scan(r, sbv, blk, group_of);
     const uint32_t slot = (uint32_t)t & (kSTasks - 1);
 #pragma unroll
     for (uint32_t i = 0; i < kSTasks; i++) q[i] = slot == i ? x : q[i];
     if constexpr ((PROBE & 2) == 0) {
-      if (j == 0) ar.SB[(((uint64_t)t * ngroups + gid) / 8) * 8 + (lane >> 3)] = sbv;
+      if (j == 0) ar.SB[(((uint64_t)t * ngroups + g0) / 8) * 8 + blk] = sbv;
     }
     if (slot == kSTasks - 1 || t + 1 == ntasks) {
       const uint64_t t0 = (uint64_t)t & ~7ull;
       if constexpr ((PROBE & 1) == 0) {
         const v4u32 lo = {q[0], q[1], q[2], q[3]}, hi = {q[4], q[5], q[6], q[7]};
-        v4u32* dst = reinterpret_cast<v4u32*>(ar.S + arena_s_word(t0, gid, j, ar.W));
+        v4u32* dst = reinterpret_cast<v4u32*>(ar.S + arena_s_word(t0, gblk, j, ar.W));
         if constexpr (ANNETY_S_NT) {
           __builtin_nontemporal_store(lo, dst);
           __builtin_nontemporal_store(hi, dst + 64);  // + 1 KiB
@@ -170,28 +198,20 @@ __device__ __forceinline__ void arena_line_pass(const uint8_t* __restrict__ base
       }
     }
   };
-  // Loads are unconditional (past the last task a group re-reads its current line, an L2 hit): with the
+  // Loads are unconditional (past the last task a wave re-reads its current superblock, an L2 hit): with the
   // next task's loads behind a branch the waitcnt pass merges the two paths and waits vmcnt(0) before
   // every fold, which serialises the A/B double buffer.
   for (int t = 0; t < ntasks; t += 2) {
     ANNETY_PRIO_HI();
-    {
-      const uint4* s = reinterpret_cast<const uint4*>(t + 1 < ntasks ? lp + pstep : lp);
-#pragma unroll
-      for (int i = 0; i < 8; i++) B[i] = s[i];
-    }
+    load(t + 1 < ntasks ? lp + pstep : lp, B);
     __builtin_amdgcn_sched_barrier(0);
     ANNETY_PRIO_LO();
-    finish(absorb_line(0u, A, k, lds), t);
+    finish(A, t);
     ANNETY_PRIO_HI();
-    {
-      const uint4* s = reinterpret_cast<const uint4*>(t + 2 < ntasks ? lp + 2 * pstep : lp);
-#pragma unroll
-      for (int i = 0; i < 8; i++) A[i] = s[i];
-    }
+    load(t + 2 < ntasks ? lp + 2 * pstep : lp, A);
     __builtin_amdgcn_sched_barrier(0);
     ANNETY_PRIO_LO();
-    if (t + 1 < ntasks) finish(absorb_line(0u, B, k, lds), t + 1);
+    if (t + 1 < ntasks) finish(B, t + 1);
     lp += 2 * pstep;
   }
 }

@@ -271,6 +271,99 @@ __global__ __launch_bounds__(BLK) void crc32_onekib_nt_kernel(const uint8_t* __r
   }
 }
 
+// G = 32 fixed batches whose length is a multiple of 4 KiB (n even; the long-payload split's 64 KiB segments
+// of config 2): crc32_fixed_kernel<32, true, false>'s rounds with coalesced nontemporal loads. A wave = two
+// lane groups (lanes 0-31 and 32-63, payloads g0 and g0 + 1); a round reads 4 KiB of each. Load i covers
+// block blk_of(i) of the wave's 8 KiB (group = bit 2, block of the 4 KiB = bits 0-1), chosen so that after
+// transpose_blocks() / fold_halves() lane l holds line j = 8 (2 l3 + l4) + (l & 7) of its own group's round:
+// the groups stay the two half-waves (group_xor_reduce<32> as before) and the join takes slot j. The round
+// register enters the chains that fold the first halves: a lane with l3 = 0 folds the first half of its own line
+// (chain a) and of its partner's (lane ^ 8, chain b), so it injects its own and the partner's register.
+template <int BLK = kBlock, int VWG = kVwg>
+__global__ __launch_bounds__(BLK) void crc32_fixed32_nt_kernel(const uint8_t* __restrict__ base, size_t n,
+                                                               size_t stride, uint32_t rounds,
+                                                               const uint4* __restrict__ img_slice,
+                                                               const uint4* __restrict__ img_group,
+                                                               uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsImageBytes / 16];
+  const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
+  const uint32_t l = threadIdx.x & 63, l3 = (l >> 3) & 1, l4 = (l >> 4) & 1;
+  const size_t gid = group_id<BLK, 32, VWG>();
+  const size_t g0 = ((size_t)__builtin_amdgcn_readfirstlane((uint32_t)(gid >> 32)) << 32) |
+                    (size_t)(__builtin_amdgcn_readfirstlane((uint32_t)gid) & ~1u);
+  const size_t ngroups = ((size_t)gridDim.x * BLK) / 32;
+  const size_t ntasks = g0 < n ? (n - 1 - g0) / ngroups + 1 : 0;  // the same for both groups (n, g0 even)
+  LaneCtx k;
+  k.L0 = (threadIdx.x & 31) << 3;
+  k.L1 = k.L0 | (1u << 16);
+  const uint32_t jl = 8 * (2 * l3 + l4) + (l & 7);  // this lane's line of the round
+  k.slot4 = jl << 2;
+  const uint32_t lane_off = coalesced_lane_offset(l);
+  const uint32_t sinit = (l & 31) == 0 ? kInit : 0u;  // line 0, half 0, chunk 0 of each payload (lanes 0, 32)
+  // load i -> block blk_of(i): group (i >> 1) & 1, block 2 (i >> 2) + (i & 1) of that group's 4 KiB
+  auto load_step = [&](size_t t, uint32_t r, uint4 (&v)[8]) __attribute__((always_inline)) {
+    const uint8_t* b0 = base + (g0 + t * ngroups) * stride + (size_t)r * 4096 + lane_off;
+    const uint8_t* b1 = b0 + stride;
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const uint8_t* a = (((i >> 1) & 1) ? b1 : b0) + 1024 * (2 * (i >> 2) + (i & 1));
+      const v4u32 x = __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(a));
+      v[i] = make_uint4(x.x, x.y, x.z, x.w);
+    }
+  };
+  uint4 A[8], B[8];
+  if (ntasks > 0) load_step(0, 0, A);
+  load_image(lds4, img_slice, img_group);
+  __syncthreads();
+
+  const size_t nsteps = ntasks * rounds;
+  size_t t_ld = 0, t_c = 0;
+  uint32_t r_ld = 0, r_c = 0;
+  auto advance = [&](size_t& t, uint32_t& r) {
+    if (++r == rounds) {
+      r = 0;
+      ++t;
+    }
+  };
+  advance(t_ld, r_ld);
+  uint32_t s = 0;
+  auto compute_step = [&](uint4 (&v)[8]) __attribute__((always_inline)) {
+    transpose_blocks(v);
+    uint32_t sin = 0;
+    if (r_c > 0) sin = nibble_map_uniform(s, lds, kLdsRoundOff);
+    const uint32_t sp = (uint32_t)__builtin_amdgcn_mov_dpp((int)sin, 0x128, 0xF, 0xF, false);  // lane ^ 8's
+    v[0].x ^= l3 ? 0u : (r_c == 0 ? sinit : sin);
+    v[4].x ^= l3 ? 0u : sp;
+    s = fold_halves(v, k, lds, l3);
+    if (r_c == rounds - 1) {
+      const uint32_t c = group_xor_reduce<32>(nibble_map_lane(s, lds, k.slot4));
+      if ((l & 31) == 31) out[g0 + (l >> 5) + t_c * ngroups] = ~c;
+      s = 0;
+    }
+    advance(t_c, r_c);
+  };
+  for (size_t q = 0; q < nsteps; q += 2) {
+    ANNETY_PRIO_HI();
+    {
+      const bool ok = q + 1 < nsteps;
+      load_step(ok ? t_ld : 0, ok ? r_ld : 0u, B);
+    }
+    advance(t_ld, r_ld);
+    __builtin_amdgcn_sched_barrier(0);
+    ANNETY_PRIO_LO();
+    compute_step(A);
+    ANNETY_PRIO_HI();
+    {
+      const bool ok = q + 2 < nsteps;
+      load_step(ok ? t_ld : 0, ok ? r_ld : 0u, A);
+    }
+    advance(t_ld, r_ld);
+    __builtin_amdgcn_sched_barrier(0);
+    ANNETY_PRIO_LO();
+    if (q + 1 < nsteps) compute_step(B);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // General kernel: any alignment, any length (variable-length batches and odd fixed shapes).
 // Lines are the 128-byte lines of ABSOLUTE device memory, so every load is aligned and never leaves
@@ -652,7 +745,8 @@ hipError_t launch_one_g(const FixedLaunch& a, hipStream_t stream) {
   return hipGetLastError();
 }
 
-// ANNETY_CRC_FIXED_NT=0 keeps contiguous 1 KiB batches on crc32_oneround_kernel<8> (A/B), read once.
+// ANNETY_CRC_FIXED_NT=0 keeps contiguous 1 KiB batches on crc32_oneround_kernel<8> and G = 32 batches on
+// crc32_fixed_kernel<32> (A/B), read once.
 bool onekib_nt_enabled() {
   static const bool on = [] {
     const char* e = std::getenv("ANNETY_CRC_FIXED_NT");
@@ -698,6 +792,15 @@ hipError_t launch_full(const FixedLaunch& a, hipStream_t stream) {
 }  // namespace
 
 hipError_t launch_fixed(const FixedLaunch& a, hipStream_t stream) {
+  if (!a.raw && a.full && a.group == 32 && a.n % 2 == 0 && a.stride % 16 == 0 && onekib_nt_enabled()) {
+    size_t blocks = (a.n * 32 + kBlock - 1) / kBlock;
+    if (blocks > a.max_blocks) blocks = a.max_blocks;
+    if (blocks == 0) return hipSuccess;
+    hipLaunchKernelGGL((crc32_fixed32_nt_kernel<>), dim3((unsigned)blocks), dim3(kBlock), 0, stream,
+                       static_cast<const uint8_t*>(a.base), a.n, a.stride, a.rounds,
+                       static_cast<const uint4*>(a.img_slice), static_cast<const uint4*>(a.img_group), a.out);
+    return hipGetLastError();
+  }
   if (!a.raw && a.full && a.rounds == 1) return launch_one(a, stream);
   if (a.raw) return a.full ? launch_full<true, true>(a, stream) : launch_full<false, true>(a, stream);
   return a.full ? launch_full<true, false>(a, stream) : launch_full<false, false>(a, stream);
