@@ -12,9 +12,9 @@
 #define RC(x) do { int r_ = (x); if (r_) { printf("%s -> %d\n", #x, r_); exit(3); } } while (0)
 using namespace annety_crc;
 
-template <int PROBE>
+template <int PROBE, bool NT = true>
 void lines(DeviceCtx&, const ArenaLaunch& a) {
-  CK(launch_arena_lines_p<PROBE>(a, 0));
+  CK((launch_arena_lines_p<PROBE, NT>(a, 0)));
 }
 
 // `arena_mb place`: the product line pass with the arena and the S/SB scratch at different offsets in
@@ -71,10 +71,16 @@ int main(int argc, char** argv) {
     printf("%-36s %.4f ms  %.1f GB/s\n", name, ms / 100, bytes / (ms / 100) / 1e6);
   };
   t([&] { RC(annety_crc32_batch_fixed(d, bytes / 1024, 1024, 1024, out, nullptr)); }, "config-1 kernel (oneround<8>)");
-  t([&] { lines<0>(*c, a); }, "arena lines (product)");
-  t([&] { lines<1>(*c, a); }, "  no S store");
-  t([&] { lines<2>(*c, a); }, "  no superblock scan");
-  t([&] { lines<3>(*c, a); }, "  no S store, no superblock scan");
+  for (int rep = 0; rep < 2; rep++) {
+    t([&] { lines<0>(*c, a); }, "arena lines (product, coalesced nt loads)");
+    t([&] { lines<1>(*c, a); }, "  no S store");
+    t([&] { lines<2>(*c, a); }, "  no superblock scan");
+    t([&] { lines<3>(*c, a); }, "  no S store, no superblock scan");
+    t([&] { lines<0, false>(*c, a); }, "arena lines, per-line loads");
+    t([&] { lines<1, false>(*c, a); }, "  no S store");
+    t([&] { lines<3, false>(*c, a); }, "  no S store, no superblock scan");
+  }
+  if (getenv("NO_SW")) return 0;
   t([&] { CK(launch_arena_lines_sw<0>(a, 0)); }, "store wave (8 + 1 waves, LDS ring)");
   t([&] { CK(launch_arena_lines_sw<1>(a, 0)); }, "  ring, store wave stores nothing");
   t([&] { CK(launch_arena_lines_sw<2>(a, 0)); }, "  no ring (9 waves, no hand-off)");
