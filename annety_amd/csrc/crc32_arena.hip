@@ -795,7 +795,7 @@ hipError_t launch_stitch_lite(const ArenaLaunch& a, const void* img_lite, size_t
 
 template <int PROBE, bool NT = true>
 hipError_t launch_arena_lines_p(const ArenaLaunch& a, hipStream_t stream) {
-  static_assert(kBlock / 8 == 64 && kSTasks == 8, "arena_geom / arena_s_word assume 64 groups per block, 8-task bursts");
+  static_assert(kBlock / 8 == 64 && kSTasks % 4 == 0, "arena_geom / arena_s_word assume 64 groups per block, bursts of 4k tasks");
   const ArenaGeom geo = arena_geom(a);
   hipLaunchKernelGGL((crc32_arena_lines_kernel<PROBE, NT>), dim3((unsigned)geo.blocks), dim3(kBlock), 0, stream,
                      reinterpret_cast<const uint8_t*>((uintptr_t)(a.fs0 * 8192)), line_out(a, geo), static_cast<const uint4*>(a.img_slice), static_cast<const uint4*>(a.img_group8),

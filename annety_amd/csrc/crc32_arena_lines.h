@@ -59,6 +59,7 @@ __device__ __forceinline__ bool extent_matches(const uint64_t* check, uint32_t p
 #ifndef ANNETY_S_NT
 #define ANNETY_S_NT 1
 #endif
+
 // NT (product 1; 0 = the per-line loads, for A/B through ANNETY_CRC_LINES_NT=0): a wave's 8 KiB superblock
 // arrives as 8 coalesced nontemporal 1 KiB loads (one per block) and transpose_blocks() / fold_halves()
 // (crc32_device.h) leave lane l with line l & 7 of block folded_block(l); lane group q = l / 8 then holds block
@@ -111,9 +112,10 @@ __device__ __forceinline__ void arena_line_pass(const uint8_t* __restrict__ base
   load_image<kLdsArenaImageBytes, BLK>(lds4, img_slice, img_group8, img_sb);
   __syncthreads();
 
-  // S of 8 consecutive tasks leaves in two 16-byte stores per lane, each 1 KiB contiguous per wave:
-  // interleaved with the read stream, a dword per lane per task cost 30 us of a 211 us pass, 16-byte
-  // quads of 4 tasks 20 (microbench/arena_mb.hip).
+  // S of kSTasks = 16 consecutive tasks leaves in four 16-byte stores per lane, each 1 KiB contiguous per
+  // wave: interleaved with the read stream, a dword per lane per task cost 30 us of a 211 us pass, 16-byte
+  // quads of 4 tasks 20; with the coalesced loads 8-task bursts cost 14-15 us of a 173 us pass, 16-task
+  // bursts 11 (170 us), 32-task bursts the same as 16 (microbench/arena_mb.hip, profiles/r03/nt/b16/).
   uint32_t q[kSTasks];
 #pragma unroll
   for (uint32_t i = 0; i < kSTasks; i++) q[i] = 0;
@@ -184,16 +186,16 @@ __device__ __forceinline__ void arena_line_pass(const uint8_t* __restrict__ base
       if (j == 0) ar.SB[(((uint64_t)t * ngroups + g0) / 8) * 8 + blk] = sbv;
     }
     if (slot == kSTasks - 1 || t + 1 == ntasks) {
-      const uint64_t t0 = (uint64_t)t & ~7ull;
+      const uint64_t t0 = (uint64_t)t & ~(uint64_t)(kSTasks - 1);
       if constexpr ((PROBE & 1) == 0) {
-        const v4u32 lo = {q[0], q[1], q[2], q[3]}, hi = {q[4], q[5], q[6], q[7]};
         v4u32* dst = reinterpret_cast<v4u32*>(ar.S + arena_s_word(t0, gblk, j, ar.W));
-        if constexpr (ANNETY_S_NT) {
-          __builtin_nontemporal_store(lo, dst);
-          __builtin_nontemporal_store(hi, dst + 64);  // + 1 KiB
-        } else {
-          dst[0] = lo;
-          dst[64] = hi;
+#pragma unroll
+        for (uint32_t b = 0; b < kSTasks / 4; b++) {  // 1 KiB apart
+          const v4u32 w = {q[4 * b], q[4 * b + 1], q[4 * b + 2], q[4 * b + 3]};
+          if constexpr (ANNETY_S_NT)
+            __builtin_nontemporal_store(w, dst + 64 * b);
+          else
+            dst[64 * b] = w;
         }
       }
     }

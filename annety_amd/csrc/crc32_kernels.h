@@ -142,15 +142,19 @@ hipError_t launch_bucket_place(const uint64_t* off, const uint32_t* len, size_t 
 
 // Line-pass layout. L line-pass workgroups of 512 lanes = W = 8L waves = 64L lane groups;
 // wave w's task t is full superblock fs0 + t*W + w (lane group g = 8w + block). Per line of a full
-// superblock the block-suffix CRC S leaves in bursts of 8 tasks, two 16-byte stores per lane that each
-// cover 1 KiB contiguously: task t of group g, line a at word
-//   ((((t / 8) * W + g / 8) * 2 + (t / 4) % 2) * 256 + ((g % 8) * 8 + a) * 4 + t % 4.
+// superblock the block-suffix CRC S leaves in bursts of K = kSTasks tasks, K / 4 16-byte stores per lane
+// that each cover 1 KiB contiguously: task t of group g, line a at word
+//   ((((t / K) * W + g / 8) * (K / 4) + (t / 4) % (K / 4)) * 256 + ((g % 8) * 8 + a) * 4 + t % 4.
 // SB (superblock suffix per block) of full superblock fs0 + i, block g at word i * 8 + g: a 128-byte line
 // holds 4 superblocks of one task (W is a multiple of 4), so no line mixes two tasks' stores. The (at
 // most two) partial superblocks keep S in S_edge[2][64] and SB in SB_edge[2][8].
-constexpr uint32_t kSTasks = 8;
+#ifndef ANNETY_S_TASKS
+#define ANNETY_S_TASKS 16
+#endif
+constexpr uint32_t kSTasks = ANNETY_S_TASKS;  // tasks per S burst (kSTasks / 4 stores of 1 KiB per wave)
 inline __host__ __device__ uint64_t arena_s_word(uint64_t t, uint64_t group, uint32_t a, uint64_t W) {
-  return ((((t >> 3) * W + (group >> 3)) * 2 + ((t >> 2) & 1)) << 8) + (((group & 7) * 8 + a) << 2) + (t & 3);
+  return ((((t / kSTasks) * W + (group >> 3)) * (kSTasks / 4) + ((t >> 2) % (kSTasks / 4))) << 8) +
+         (((group & 7) * 8 + a) << 2) + (t & 3);
 }
 
 // Geometry of one arena call: the line pass on `blocks` workgroups, and the scratch layout
@@ -159,7 +163,7 @@ struct ArenaGeom {
   size_t blocks;         // line-pass workgroups L
   uint64_t W;            // line-pass waves = 8L
   uint64_t ntasks;       // tasks of the busiest wave
-  uint64_t nbursts;      // ceil(ntasks / 8)
+  uint64_t nbursts;      // ceil(ntasks / kSTasks)
   uint64_t sb_off, edge_off, words;
 };
 inline ArenaGeom arena_geom(const ArenaLaunch& a, size_t line_blocks) {  // line_blocks >= 1
@@ -169,7 +173,7 @@ inline ArenaGeom arena_geom(const ArenaLaunch& a, size_t line_blocks) {  // line
   g.W = 8 * (uint64_t)g.blocks;
   g.ntasks = (nsbf + g.W - 1) / g.W;
   g.nbursts = (g.ntasks + kSTasks - 1) / kSTasks;
-  g.sb_off = g.nbursts * g.W * 512;
+  g.sb_off = g.nbursts * g.W * 64 * kSTasks;
   g.edge_off = g.sb_off + nsbf * 8;
   g.words = g.edge_off + 144;
   return g;
