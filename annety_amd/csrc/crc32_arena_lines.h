@@ -49,8 +49,8 @@ __device__ __forceinline__ bool extent_matches(const uint64_t* check, uint32_t p
   return l == lo && h == hi && b == 0;
 }
 
-//   PROBE (microbench only; product = 0): bit 0 drops the S stores, bit 1 the superblock scan - wrong
-//   outputs, used to measure what those stages cost.
+//   PROBE (microbench only; product = 0): bit 0 drops the S stores, bit 1 the superblock scan, bit 2 only
+//   the SB stores - wrong outputs, used to measure what those stages cost.
 // `base` = the first full superblock (fs0 * 8192), passed as its own kernel argument: loads through a
 // __restrict__ kernel-argument pointer compile to the config-1 kernel's schedule; the same loads through
 // integer-built address-space-1 pointers ran this pass 30 % slower (microbench/arena_mb.hip).
@@ -182,7 +182,7 @@ __device__ __forceinline__ void arena_line_pass(const uint8_t* __restrict__ base
     const uint32_t slot = (uint32_t)t & (kSTasks - 1);
 #pragma unroll
     for (uint32_t i = 0; i < kSTasks; i++) q[i] = slot == i ? x : q[i];
-    if constexpr ((PROBE & 2) == 0) {
+    if constexpr ((PROBE & 6) == 0) {
       if (j == 0) ar.SB[(((uint64_t)t * ngroups + g0) / 8) * 8 + blk] = sbv;
     }
     if (slot == kSTasks - 1 || t + 1 == ntasks) {

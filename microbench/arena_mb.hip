@@ -76,6 +76,8 @@ int main(int argc, char** argv) {
     t([&] { lines<1>(*c, a); }, "  no S store");
     t([&] { lines<2>(*c, a); }, "  no superblock scan");
     t([&] { lines<3>(*c, a); }, "  no S store, no superblock scan");
+    t([&] { lines<4>(*c, a); }, "  no SB store");
+    t([&] { lines<5>(*c, a); }, "  no S store, no SB store");
     t([&] { lines<0, false>(*c, a); }, "arena lines, per-line loads");
     t([&] { lines<1, false>(*c, a); }, "  no S store");
     t([&] { lines<3, false>(*c, a); }, "  no S store, no superblock scan");
