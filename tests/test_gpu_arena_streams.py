@@ -19,7 +19,7 @@ def _batch(seed: int, total: int):
     lens = []
     s = 0
     while s < total:
-        L = int(min(65536, 64 * rng.zipf(1.6) + rng.integers(0, 64)))
+        L = int(min(65536, 64 * min(int(rng.zipf(1.6)), 1 << 20) + rng.integers(0, 64)))
         lens.append(L)
         s += L
     lens = np.array(lens, dtype=np.int64)

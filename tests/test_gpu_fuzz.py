@@ -18,7 +18,8 @@ def _lengths(rng, n):
     if kind == 0:
         return rng.integers(0, 200, n)
     if kind == 1:
-        return np.minimum(200_000, 64 * rng.zipf(1.3, n) + rng.integers(0, 64, n))
+        # zipf draws reach 1e17 and more: clip before scaling, or 64 * z wraps negative
+        return np.minimum(200_000, 64 * np.minimum(rng.zipf(1.3, n), 1 << 20) + rng.integers(0, 64, n))
     if kind == 2:
         return rng.integers(0, 20_000, n)
     out = rng.integers(1, 5000, n)

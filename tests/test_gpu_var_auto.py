@@ -13,7 +13,7 @@ pytestmark = pytest.mark.gpu
 
 def _packed(seed, n, gap=0):
     rng = np.random.default_rng(seed)
-    lens = np.minimum(65536, 64 * rng.zipf(1.3, n) + rng.integers(0, 64, n)).astype(np.int64)
+    lens = np.minimum(65536, 64 * np.minimum(rng.zipf(1.3, n), 1 << 20) + rng.integers(0, 64, n)).astype(np.int64)
     offs = np.concatenate([[0], np.cumsum(lens + gap)[:-1]]).astype(np.int64)
     data = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 256, dtype=np.uint8)
     return data, offs, lens
@@ -130,7 +130,7 @@ def test_sorted_calls_back_to_back(gpu):
     for i in range(10):
         n = 700 + 37 * i if i % 2 == 0 else 2500 + 301 * i
         rng = np.random.default_rng(100 + i)
-        lens = np.minimum(40000, 64 * rng.zipf(1.4, n) + rng.integers(0, 300, n)).astype(np.int64)
+        lens = np.minimum(40000, 64 * np.minimum(rng.zipf(1.4, n), 1 << 20) + rng.integers(0, 300, n)).astype(np.int64)
         lens[rng.integers(0, n, n // 20)] = 0
         offs = np.concatenate([[0], np.cumsum(lens + 5000)[:-1]]).astype(np.int64)
         perm = rng.permutation(n)  # unsorted descriptors
