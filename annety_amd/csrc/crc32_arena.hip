@@ -520,7 +520,7 @@ __global__ __launch_bounds__(kBlock) void crc32_arena_lines_kernel(const uint8_t
                                                                    const uint4* __restrict__ img_slice,
                                                                    const uint4* __restrict__ img_group8,
                                                                    const uint4* __restrict__ img_sb) {
-  __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsArenaImageBytes / 16];
+  __shared__ __attribute__((aligned(16))) uint4 lds4[(NT ? kLdsArenaNtImageBytes : kLdsArenaImageBytes) / 16];
   arena_line_pass<PROBE, NT>(base, ar, blockIdx.x, gridDim.x, lds4, img_slice, img_group8, img_sb);
 }
 

@@ -109,7 +109,7 @@ __device__ __forceinline__ void arena_line_pass(const uint8_t* __restrict__ base
   };
   uint4 A[8], B[8];
   if (ntasks > 0) load(lp, A);
-  load_image<kLdsArenaImageBytes, BLK>(lds4, img_slice, img_group8, img_sb);
+  load_image<NT ? kLdsArenaNtImageBytes : kLdsArenaImageBytes, BLK>(lds4, img_slice, img_group8, img_sb);
   __syncthreads();
 
   // S of kSTasks = 16 consecutive tasks leaves in four 16-byte stores per lane, each 1 KiB contiguous per
@@ -173,7 +173,7 @@ __device__ __forceinline__ void arena_line_pass(const uint8_t* __restrict__ base
     uint32_t r;
     if constexpr (NT) {
       transpose_blocks(v);
-      r = fold_halves(v, k, lds, (lane >> 3) & 1);
+      r = fold_halves(v, k, lds, (lane >> 3) & 1, kLdsArenaImageBytes);
     } else {
       r = absorb_line(0u, v, k, lds);
     }

@@ -209,7 +209,7 @@ struct HostImages {
   std::vector<uint32_t> slice;   // common part: slicing tables (32768 words) + half-line join (128 words)
   std::vector<uint32_t> groups;  // kNumGroups * (kGroupImageBytes / 4)
   std::vector<uint32_t> unshift; // 24 maps x 128 words (U_lo[0..15], U_hi[0..7])
-  std::vector<uint32_t> sb;      // arena superblock join: (k, v, g) = shift_{(7-g)*1024}(v << 4k)
+  std::vector<uint32_t> sb;      // arena superblock join: (k, v, g) = shift_{(7-g)*1024}(v << 4k); byte map
   std::vector<uint32_t> stitch;  // arena stitch: segment maps F/G/UL/UB, unshift, shift_32 (crc32_math.h)
 };
 
@@ -291,7 +291,13 @@ const HostImages& host_images() {
       nibble_tables(acc, img.unshift.data() + (16 + h) * 128);
       acc = gf2_mul(inv16, acc);
     }
-    img.sb.assign(kLdsSbJoinBytes / 4, 0);
+    img.sb.assign((kLdsSbJoinBytes + kLdsByteMapBytes) / 4, 0);
+    {  // then the half-line join as byte tables: B_k[e] = shift_64(e << 8k) (crc32_device.h byte_map64)
+      const Gf2Mat m = shift_matrix(64);
+      uint32_t* bm = img.sb.data() + kLdsSbJoinBytes / 4;
+      for (uint32_t kk = 0; kk < 4; kk++)
+        for (uint32_t e = 0; e < 256; e++) bm[kk * 256 + e] = gf2_apply(m, e << (8 * kk));
+    }
     for (uint32_t g = 0; g < 8; g++) {
       uint32_t nt[8 * 16];
       nibble_tables(shift_matrix((uint64_t)(7 - g) * 1024), nt);
@@ -527,6 +533,7 @@ int run_fixed(DeviceCtx& c, const void* d_base, size_t n, size_t len, size_t str
   a.raw = raw;
   a.img_slice = c.d_slice;
   a.img_group = group_image(c, a.group);
+  a.img_bytemap = static_cast<const char*>(c.d_sb) + kLdsSbJoinBytes;
   if (raw) {
     const Gf2Mat m = shift_matrix(len);
     std::memcpy(a.raw_shift_cols.c, m.col, sizeof m.col);

@@ -253,12 +253,19 @@ __device__ __forceinline__ void transpose_blocks(uint4 (&v)[8]) {
   swap_stage<1>(v);
   swap_stage<2>(v);
 }
+// shift_64 through the byte tables at LDS byte offset `off` (kLdsByteMapBytes): 4 lookups at 2 VALU per
+// address against the nibble map's 8; the lanes' random bytes cost 3-4-way bank conflicts, which the LDS
+// has room for. microbench/bytemap_mb.hip: config 1 172.5-175.0 us against 175.6-179.9 with the nibble map.
+__device__ __forceinline__ uint32_t byte_map64(uint32_t x, const uint32_t* lds, uint32_t off) {
+  const uint32_t* t = lds + off / 4;
+  return xor3(t[x & 255], t[256 + ((x >> 8) & 255)], t[512 + ((x >> 16) & 255)]) ^ t[768 + (x >> 24)];
+}
 // After transpose_blocks: the raw CRC (register 0) of line l & 7 of block 4 l3 + 2 l5 + l4. The two 64-byte
 // chains v[0..3] and v[4..7] are half l3 of two lines; the halves meet across lane bit 3 (DPP row_ror:8 =
 // lane ^ 8): lanes with l3 = 0 keep their first block's line, lanes with l3 = 1 their second block's,
-// raw(line) = shift_64(raw(first half)) ^ raw(second half).
+// raw(line) = shift_64(raw(first half)) ^ raw(second half), shift_64 from the byte tables at `bm_off`.
 __device__ __forceinline__ uint32_t fold_halves(const uint4 (&v)[8], const LaneCtx& k, const uint32_t* lds,
-                                                uint32_t l3) {
+                                                uint32_t l3, uint32_t bm_off) {
   uint32_t xa = v[0].x, xb = v[4].x;
 #pragma unroll
   for (int i = 0; i < 4; i++) {
@@ -270,7 +277,7 @@ __device__ __forceinline__ uint32_t fold_halves(const uint4 (&v)[8], const LaneC
   const uint32_t send = l3 ? xa : xb;
   const uint32_t got = (uint32_t)__builtin_amdgcn_mov_dpp((int)send, 0x128, 0xF, 0xF, false);
   const uint32_t first = l3 ? got : xa, second = l3 ? xb : got;
-  return nibble_map_uniform(first, lds, kLdsHalfOff) ^ second;
+  return byte_map64(first, lds, bm_off) ^ second;
 }
 // Block of a lane's line after fold_halves.
 __device__ __forceinline__ uint32_t folded_block(uint32_t l) {

@@ -23,6 +23,7 @@ struct FixedLaunch {
   bool raw;                // crc32_update semantics (out holds the input register, in place)
   const void* img_slice;   // 128 KiB slicing-table image (device)
   const void* img_group;   // 16.5 KiB join + round image for `group` (device)
+  const void* img_bytemap; // kLdsByteMapBytes of half-line join byte tables (the nontemporal kernels)
   ShiftCols raw_shift_cols;  // raw only: shift_len columns
   uint32_t* out;           // digests (device)
   size_t max_blocks;       // persistent grid size (one workgroup per CU)
@@ -88,7 +89,7 @@ struct ArenaLaunch {
   uint32_t* scratch;         // arena_geom(*this).words words (device)
   const void* img_slice;     // common image part (slicing tables + half-line join)
   const void* img_group8;    // G = 8 group part (lane join + round maps)
-  const void* img_sb;        // superblock join, kLdsSbJoinBytes
+  const void* img_sb;        // superblock join, kLdsSbJoinBytes, then the half-line join byte tables
   const void* img_stitch;    // stitch maps, kLdsStitchImageBytes - kLdsCommonBytes
   const void* zero_line;     // 128 zero bytes (device), read in place of lines outside the arena
   uint32_t* out;             // digests, or (update) registers in place

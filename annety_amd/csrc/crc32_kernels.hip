@@ -217,8 +217,9 @@ template <int BLK = kBlock, int VWG = kVwg>
 __global__ __launch_bounds__(BLK) void crc32_onekib_nt_kernel(const uint8_t* __restrict__ base, size_t n,
                                                               const uint4* __restrict__ img_slice,
                                                               const uint4* __restrict__ img_group,
+                                                              const uint4* __restrict__ img_bytemap,
                                                               uint32_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsImageBytes / 16];
+  __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsFixedNtImageBytes / 16];
   const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
   const uint32_t l = threadIdx.x & 63, j = l & 7, l3 = (l >> 3) & 1;
   const size_t gid = group_id<BLK, 8, VWG>();
@@ -245,13 +246,14 @@ __global__ __launch_bounds__(BLK) void crc32_onekib_nt_kernel(const uint8_t* __r
   };
   uint4 A[8], B[8];
   if (ntasks > 0) load(wp, A);
-  load_image<kLdsImageBytes, BLK>(lds4, img_slice, img_group);
+  load_image<kLdsFixedNtImageBytes, BLK, kLdsImageBytes>(lds4, img_slice, img_group, img_bytemap);
   __syncthreads();
   auto finish = [&](uint4 (&v)[8]) __attribute__((always_inline)) {
     transpose_blocks(v);
     v[0].x ^= sinit;
     v[4].x ^= sinit;
-    const uint32_t c = group_xor_reduce<8>(nibble_map_lane(fold_halves(v, k, lds, l3), lds, k.slot4));
+    const uint32_t c =
+        group_xor_reduce<8>(nibble_map_lane(fold_halves(v, k, lds, l3, kLdsImageBytes), lds, k.slot4));
     if (j == 7) *op = ~c;
     op += ngroups;
   };
@@ -284,8 +286,9 @@ __global__ __launch_bounds__(BLK) void crc32_fixed32_nt_kernel(const uint8_t* __
                                                                size_t stride, uint32_t rounds,
                                                                const uint4* __restrict__ img_slice,
                                                                const uint4* __restrict__ img_group,
+                                                               const uint4* __restrict__ img_bytemap,
                                                                uint32_t* __restrict__ out) {
-  __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsImageBytes / 16];
+  __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsFixedNtImageBytes / 16];
   const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
   const uint32_t l = threadIdx.x & 63, l3 = (l >> 3) & 1, l4 = (l >> 4) & 1;
   const size_t gid = group_id<BLK, 32, VWG>();
@@ -313,7 +316,7 @@ __global__ __launch_bounds__(BLK) void crc32_fixed32_nt_kernel(const uint8_t* __
   };
   uint4 A[8], B[8];
   if (ntasks > 0) load_step(0, 0, A);
-  load_image(lds4, img_slice, img_group);
+  load_image<kLdsFixedNtImageBytes, BLK, kLdsImageBytes>(lds4, img_slice, img_group, img_bytemap);
   __syncthreads();
 
   const size_t nsteps = ntasks * rounds;
@@ -334,7 +337,7 @@ __global__ __launch_bounds__(BLK) void crc32_fixed32_nt_kernel(const uint8_t* __
     const uint32_t sp = (uint32_t)__builtin_amdgcn_mov_dpp((int)sin, 0x128, 0xF, 0xF, false);  // lane ^ 8's
     v[0].x ^= l3 ? 0u : (r_c == 0 ? sinit : sin);
     v[4].x ^= l3 ? 0u : sp;
-    s = fold_halves(v, k, lds, l3);
+    s = fold_halves(v, k, lds, l3, kLdsImageBytes);
     if (r_c == rounds - 1) {
       const uint32_t c = group_xor_reduce<32>(nibble_map_lane(s, lds, k.slot4));
       if ((l & 31) == 31) out[g0 + (l >> 5) + t_c * ngroups] = ~c;
@@ -762,7 +765,7 @@ hipError_t launch_one(const FixedLaunch& a, hipStream_t stream) {
     if (blocks == 0) return hipSuccess;
     hipLaunchKernelGGL((crc32_onekib_nt_kernel<>), dim3((unsigned)blocks), dim3(kBlock), 0, stream,
                        static_cast<const uint8_t*>(a.base), a.n, static_cast<const uint4*>(a.img_slice),
-                       static_cast<const uint4*>(a.img_group), a.out);
+                       static_cast<const uint4*>(a.img_group), static_cast<const uint4*>(a.img_bytemap), a.out);
     return hipGetLastError();
   }
   switch (a.group) {
@@ -798,7 +801,8 @@ hipError_t launch_fixed(const FixedLaunch& a, hipStream_t stream) {
     if (blocks == 0) return hipSuccess;
     hipLaunchKernelGGL((crc32_fixed32_nt_kernel<>), dim3((unsigned)blocks), dim3(kBlock), 0, stream,
                        static_cast<const uint8_t*>(a.base), a.n, a.stride, a.rounds,
-                       static_cast<const uint4*>(a.img_slice), static_cast<const uint4*>(a.img_group), a.out);
+                       static_cast<const uint4*>(a.img_slice), static_cast<const uint4*>(a.img_group),
+                       static_cast<const uint4*>(a.img_bytemap), a.out);
     return hipGetLastError();
   }
   if (!a.raw && a.full && a.rounds == 1) return launch_one(a, stream);

@@ -115,6 +115,12 @@ constexpr uint32_t kChunkBytes = 128;  // one cache line per lane per round
 constexpr uint32_t kLdsSbJoinOff = kLdsImageBytes;
 constexpr uint32_t kLdsSbJoinBytes = 4096;
 constexpr uint32_t kLdsArenaImageBytes = kLdsSbJoinOff + kLdsSbJoinBytes;  // 152576
+// Half-line join as byte tables for the coalesced nontemporal kernels (crc32_device.h fold_halves): 4 tables
+// x 256 words, B_k[e] = shift_64(e << 8k), after the fixed image or after the arena image (the device buffer
+// holding the superblock join holds it right behind, so the arena stages both in one piece).
+constexpr uint32_t kLdsByteMapBytes = 4096;
+constexpr uint32_t kLdsFixedNtImageBytes = kLdsImageBytes + kLdsByteMapBytes;     // 152576
+constexpr uint32_t kLdsArenaNtImageBytes = kLdsArenaImageBytes + kLdsByteMapBytes;  // 156672
 // Arena path, stitch kernel: common + segment maps + inverse shifts + quarter-line join (no group part)
 //   [kLdsMapOff, +16 KiB)  set of 32 maps, (k, i, v) at (k*32 + i)*64 + v*4: i = m-1: F(m) = shift_{128m}
 //                          (m = 1..8), 7+m: G(m) = shift_{1024m}, 16+q: UL(q) = shift_{-128q},
