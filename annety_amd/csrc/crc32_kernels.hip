@@ -2,9 +2,10 @@
 //
 // Shape of the hot kernel:
 //   * one workgroup of 512 lanes per CU (the 144.5 KiB LDS image leaves room for exactly one);
-//   * a payload is owned by a lane-group of G lanes (G = 1..32); per round each lane reads one
-//     128-byte line (8 back-to-back global_load_dwordx4), so a wave streams G*128*64/G = 8 KiB of
-//     contiguous payload per round - the access shape that reaches the HBM roof on this chip;
+//   * a payload is owned by a lane-group of G lanes (G = 1..32); per round each lane folds one 128-byte
+//     line, and a wave streams 8 KiB of contiguous payload per round. The per-line kernels read a lane's
+//     line as 8 back-to-back global_load_dwordx4; the nontemporal kernels (crc32_onekib_nt_kernel,
+//     crc32_fixed32_nt_kernel) read 8 coalesced 1 KiB pieces and transpose them in registers;
 //   * each lane folds its line through slicing-by-4 tables held in LDS as 32-way replicated paired
 //     slots: one v_perm_b32 builds the address, one ds_read_b64 fetches two tables, no bank conflicts;
 //   * lanes' partial registers are re-joined with the linear map shift_{(G-1-j)*128} (LDS nibble
