@@ -220,6 +220,7 @@ __global__ __launch_bounds__(BLK) void crc32_onekib_nt_kernel(const uint8_t* __r
                                                               const uint4* __restrict__ img_group,
                                                               const uint4* __restrict__ img_bytemap,
                                                               uint32_t* __restrict__ out) {
+  static_assert(BLK % 64 == 0 && (VWG == 0 || VWG % 64 == 0), "a wave's lanes must be 8 consecutive lane groups");
   __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsFixedNtImageBytes / 16];
   const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
   const uint32_t l = threadIdx.x & 63, j = l & 7, l3 = (l >> 3) & 1;
@@ -289,6 +290,7 @@ __global__ __launch_bounds__(BLK) void crc32_fixed32_nt_kernel(const uint8_t* __
                                                                const uint4* __restrict__ img_group,
                                                                const uint4* __restrict__ img_bytemap,
                                                                uint32_t* __restrict__ out) {
+  static_assert(BLK % 64 == 0 && (VWG == 0 || VWG % 64 == 0), "a wave's lanes must be 2 consecutive lane groups");
   __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsFixedNtImageBytes / 16];
   const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
   const uint32_t l = threadIdx.x & 63, l3 = (l >> 3) & 1, l4 = (l >> 4) & 1;
