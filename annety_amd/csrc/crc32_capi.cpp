@@ -291,12 +291,16 @@ const HostImages& host_images() {
       nibble_tables(acc, img.unshift.data() + (16 + h) * 128);
       acc = gf2_mul(inv16, acc);
     }
-    img.sb.assign((kLdsSbJoinBytes + kLdsByteMapBytes) / 4, 0);
-    {  // then the half-line join as byte tables: B_k[e] = shift_64(e << 8k) (crc32_device.h byte_map64)
-      const Gf2Mat m = shift_matrix(64);
-      uint32_t* bm = img.sb.data() + kLdsSbJoinBytes / 4;
-      for (uint32_t kk = 0; kk < 4; kk++)
-        for (uint32_t e = 0; e < 256; e++) bm[kk * 256 + e] = gf2_apply(m, e << (8 * kk));
+    img.sb.assign((kLdsSbJoinBytes + 2 * kLdsByteMapBytes) / 4, 0);
+    {  // then byte tables B_k[e] = shift(e << 8k) (crc32_device.h byte_map64): the half-line join shift_64,
+       // and the G = 32 round advance shift_{31*128} (crc32_fixed32_nt_kernel)
+      const uint64_t shifts[2] = {64, 31 * kChunkBytes};
+      for (int m_i = 0; m_i < 2; m_i++) {
+        const Gf2Mat m = shift_matrix(shifts[m_i]);
+        uint32_t* bm = img.sb.data() + (kLdsSbJoinBytes + m_i * kLdsByteMapBytes) / 4;
+        for (uint32_t kk = 0; kk < 4; kk++)
+          for (uint32_t e = 0; e < 256; e++) bm[kk * 256 + e] = gf2_apply(m, e << (8 * kk));
+      }
     }
     for (uint32_t g = 0; g < 8; g++) {
       uint32_t nt[8 * 16];

@@ -256,6 +256,7 @@ __device__ __forceinline__ void transpose_blocks(uint4 (&v)[8]) {
 // shift_64 through the byte tables at LDS byte offset `off` (kLdsByteMapBytes): 4 lookups at 2 VALU per
 // address against the nibble map's 8; the lanes' random bytes cost 3-4-way bank conflicts, which the LDS
 // has room for. microbench/bytemap_mb.hip: config 1 172.5-175.0 us against 175.6-179.9 with the nibble map.
+// (The same 4-table form serves any shift whose byte tables sit at `off`: crc32_fixed32_nt_kernel's round map.)
 __device__ __forceinline__ uint32_t byte_map64(uint32_t x, const uint32_t* lds, uint32_t off) {
   const uint32_t* t = lds + off / 4;
   return xor3(t[x & 255], t[256 + ((x >> 8) & 255)], t[512 + ((x >> 16) & 255)]) ^ t[768 + (x >> 24)];

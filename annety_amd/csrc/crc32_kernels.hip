@@ -291,7 +291,7 @@ __global__ __launch_bounds__(BLK) void crc32_fixed32_nt_kernel(const uint8_t* __
                                                                const uint4* __restrict__ img_bytemap,
                                                                uint32_t* __restrict__ out) {
   static_assert(BLK % 64 == 0 && (VWG == 0 || VWG % 64 == 0), "a wave's lanes must be 2 consecutive lane groups");
-  __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsFixedNtImageBytes / 16];
+  __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsFixed32NtImageBytes / 16];
   const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
   const uint32_t l = threadIdx.x & 63, l3 = (l >> 3) & 1, l4 = (l >> 4) & 1;
   const size_t gid = group_id<BLK, 32, VWG>();
@@ -319,7 +319,7 @@ __global__ __launch_bounds__(BLK) void crc32_fixed32_nt_kernel(const uint8_t* __
   };
   uint4 A[8], B[8];
   if (ntasks > 0) load_step(0, 0, A);
-  load_image<kLdsFixedNtImageBytes, BLK, kLdsImageBytes>(lds4, img_slice, img_group, img_bytemap);
+  load_image<kLdsFixed32NtImageBytes, BLK, kLdsImageBytes>(lds4, img_slice, img_group, img_bytemap);
   __syncthreads();
 
   const size_t nsteps = ntasks * rounds;
@@ -336,7 +336,7 @@ __global__ __launch_bounds__(BLK) void crc32_fixed32_nt_kernel(const uint8_t* __
   auto compute_step = [&](uint4 (&v)[8]) __attribute__((always_inline)) {
     transpose_blocks(v);
     uint32_t sin = 0;
-    if (r_c > 0) sin = nibble_map_uniform(s, lds, kLdsRoundOff);
+    if (r_c > 0) sin = byte_map64(s, lds, kLdsFixedNtImageBytes);  // shift_{31*128}
     const uint32_t sp = (uint32_t)__builtin_amdgcn_mov_dpp((int)sin, 0x128, 0xF, 0xF, false);  // lane ^ 8's
     v[0].x ^= l3 ? 0u : (r_c == 0 ? sinit : sin);
     v[4].x ^= l3 ? 0u : sp;

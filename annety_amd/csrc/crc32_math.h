@@ -120,6 +120,9 @@ constexpr uint32_t kLdsArenaImageBytes = kLdsSbJoinOff + kLdsSbJoinBytes;  // 15
 // holding the superblock join holds it right behind, so the arena stages both in one piece).
 constexpr uint32_t kLdsByteMapBytes = 4096;
 constexpr uint32_t kLdsFixedNtImageBytes = kLdsImageBytes + kLdsByteMapBytes;     // 152576
+// G = 32 rounds (crc32_fixed32_nt_kernel): the round advance shift_{31*128} as byte tables too, after the
+// half-line join's
+constexpr uint32_t kLdsFixed32NtImageBytes = kLdsFixedNtImageBytes + kLdsByteMapBytes;  // 156672
 constexpr uint32_t kLdsArenaNtImageBytes = kLdsArenaImageBytes + kLdsByteMapBytes;  // 156672
 // Arena path, stitch kernel: common + segment maps + inverse shifts + quarter-line join (no group part)
 //   [kLdsMapOff, +16 KiB)  set of 32 maps, (k, i, v) at (k*32 + i)*64 + v*4: i = m-1: F(m) = shift_{128m}
