@@ -1691,12 +1691,15 @@ int annety_pbc_encode_batch(const void* d_src, const uint64_t* d_src_off, const 
 // header walk - a dependent chain of one header read per frame, ~140-170 ns a frame from DRAM - runs on
 // its own walker thread (connections are independent), while the buffers are packed into pinned memory
 // and uploaded (pinned buffers, e.g. annety_crc_host_register'ed NetBuffer arenas, are DMA'd in place).
-// Pageable frame buffers: uploaded by the runtime's own pageable copy (1) or packed into the pinned ring by
-// the pack threads (0, ANNETY_CRC_FRAMES_PACK=1). Read once.
+// Pageable frame buffers: packed into the library's pinned ring by the pack threads (default), or uploaded by
+// the runtime's own pageable copy (ANNETY_CRC_FRAMES_PACK=0). The runtime pins a large pageable source for
+// the length of its copy; K receive buffers allocated next to each other can share a page, and two such copies
+// in flight then pin and unpin the same page - the suspected cause of the intermittent illegal address in
+// the K-connection test. The pack never hands a user page to the DMA engine. Read once.
 static bool frames_pageable_direct() {
   static const bool direct = [] {
     const char* e = std::getenv("ANNETY_CRC_FRAMES_PACK");
-    return !(e && e[0] == '1');
+    return e && e[0] == '0';
   }();
   return direct;
 }
