@@ -205,7 +205,9 @@ struct Stitcher {
   __device__ __forceinline__ uint32_t sb_addr(uint64_t sbr, uint32_t gg) const {
     const uint64_t sb = g.sb0 + sbr;
     const bool edge = sb < g.fs0 || sb >= g.fs1;
-    const uint32_t full = g.sb_word + (uint32_t)(sb - g.fs0) * 8 + gg;
+    const uint32_t r = (uint32_t)(sb - g.fs0);                                     // superblock of the full range
+    const uint32_t t = (uint32_t)(((uint64_t)(r >> 3) * g.Lmagic) >> 40);          // task = r / W = (r / 8) / L
+    const uint32_t full = g.sb_word + (uint32_t)arena_sb_word(t, r - t * 8 * g.L, gg, g.W);  // wave = r - t W
     const uint32_t ed = g.edge_word + 128u + (sb == g.sb0 ? 0u : 8u) + gg;
     return edge ? ed : full;
   }

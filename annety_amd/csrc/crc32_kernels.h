@@ -157,6 +157,12 @@ inline __host__ __device__ uint64_t arena_s_word(uint64_t t, uint64_t group, uin
   return ((((t / kSTasks) * W + (group >> 3)) * (kSTasks / 4) + ((t >> 2) % (kSTasks / 4))) << 8) +
          (((group & 7) * 8 + a) << 2) + (t & 3);
 }
+// SB in the same bursts: a wave's kSTasks SB words per block leave in one 8-byte store per lane (lane j of
+// the group holding block b keeps tasks 2j and 2j + 1), 512 bytes contiguous per wave:
+// [burst][wave][block b][task % kSTasks].
+inline __host__ __device__ uint64_t arena_sb_word(uint64_t t, uint64_t wave, uint32_t b, uint64_t W) {
+  return (((t / kSTasks) * W + wave) * 8 + b) * kSTasks + (t % kSTasks);
+}
 
 // Geometry of one arena call: the line pass on `blocks` workgroups, and the scratch layout
 // [S | SB | S_edge 128 | SB_edge 16].
@@ -175,7 +181,7 @@ inline ArenaGeom arena_geom(const ArenaLaunch& a, size_t line_blocks) {  // line
   g.ntasks = (nsbf + g.W - 1) / g.W;
   g.nbursts = (g.ntasks + kSTasks - 1) / kSTasks;
   g.sb_off = g.nbursts * g.W * 64 * kSTasks;
-  g.edge_off = g.sb_off + nsbf * 8;
+  g.edge_off = g.sb_off + g.nbursts * g.W * 8 * kSTasks;
   g.words = g.edge_off + 144;
   return g;
 }
