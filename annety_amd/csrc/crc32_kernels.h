@@ -146,9 +146,8 @@ hipError_t launch_bucket_place(const uint64_t* off, const uint32_t* len, size_t 
 // superblock the block-suffix CRC S leaves in bursts of K = kSTasks tasks, K / 4 16-byte stores per lane
 // that each cover 1 KiB contiguously: task t of group g, line a at word
 //   ((((t / K) * W + g / 8) * (K / 4) + (t / 4) % (K / 4)) * 256 + ((g % 8) * 8 + a) * 4 + t % 4.
-// SB (superblock suffix per block) of full superblock fs0 + i, block g at word i * 8 + g: a 128-byte line
-// holds 4 superblocks of one task (W is a multiple of 4), so no line mixes two tasks' stores. The (at
-// most two) partial superblocks keep S in S_edge[2][64] and SB in SB_edge[2][8].
+// SB (superblock suffix per block) in the same bursts, arena_sb_word below. The (at most two) partial
+// superblocks keep S in S_edge[2][64] and SB in SB_edge[2][8].
 #ifndef ANNETY_S_TASKS
 #define ANNETY_S_TASKS 16
 #endif
