@@ -212,6 +212,22 @@ struct Stitcher {
     return edge ? ed : full;
   }
 
+  // SB[., 0] word indices of the whole superblocks mid_s .. mid_s + 7 (relative to sb0; the first n used, the
+  // rest 0): one task division, then a wave step per superblock that wraps into the next task at most once
+  // (W >= 8). Whole superblocks between two partial ones are never the arena's edge superblocks.
+  __device__ __forceinline__ void mid_addrs(uint32_t mid_s, uint32_t n, uint32_t (&a)[8]) const {
+    const uint32_t r = (uint32_t)(g.sb0 + mid_s - g.fs0);
+    const uint32_t t = (uint32_t)(((uint64_t)(r >> 3) * g.Lmagic) >> 40);
+    const uint32_t W = (uint32_t)g.W, w = r - t * W;
+#pragma unroll
+    for (uint32_t q = 0; q < 8; q++) {
+      const uint32_t wq = w + q;
+      const bool wrap = wq >= W;
+      const uint32_t tq = t + (wrap ? 1u : 0u), wv = wrap ? wq - W : wq;
+      a[q] = q < n ? g.sb_word + ((tq / kSTasks) * W + wv) * 8 * kSTasks + tq % kSTasks : 0u;
+    }
+  }
+
   // Phase A: descriptor, plan, window and register loads (nothing the line pass writes).
   __device__ __forceinline__ void plan_a(size_t p, Plan& y, Vals& v) const { plan_a(p, g.len[p], g.off[p], y, v); }
   __device__ __forceinline__ void plan_a(size_t p, uint32_t len, uint64_t off, Plan& y, Vals& v) const {
@@ -294,8 +310,10 @@ struct Stitcher {
       v.x[q] = word(on ? y.xa[q] : dummy);
       v.y[q] = word(on && !((y.yzero >> q) & 1u) ? y.ya[q] : dummy);
     }
+    uint32_t ma[8];
+    mid_addrs(y.mid_s, y.nmid, ma);  // (dummy = 0)
 #pragma unroll
-    for (int q = 0; q < 8; q++) v.mid[q] = word((uint32_t)q < y.nmid ? sb_addr(y.mid_s + q, 0) : dummy);
+    for (int q = 0; q < 8; q++) v.mid[q] = word(ma[q]);
   }
 
   __device__ __forceinline__ void process(size_t p, const Plan& y, Vals& v) const {
@@ -342,8 +360,10 @@ struct Stitcher {
         // whole superblocks between the partial ones: acc = shift_8KiB(acc) ^ SB[s,0]
         for (uint32_t i = 0; i < y.nmid; i += 8) {
           if (i > 0) {
+            uint32_t ma[8];
+            mid_addrs(y.mid_s + i, y.nmid - i, ma);
 #pragma unroll
-            for (int q = 0; q < 8; q++) v.mid[q] = word(sb_addr(y.mid_s + (i + q < y.nmid ? i + q : i), 0));
+            for (int q = 0; q < 8; q++) v.mid[q] = word(ma[q]);
           }
 #pragma unroll
           for (int q = 0; q < 8; q++)
