@@ -205,27 +205,18 @@ struct Stitcher {
   __device__ __forceinline__ uint32_t sb_addr(uint64_t sbr, uint32_t gg) const {
     const uint64_t sb = g.sb0 + sbr;
     const bool edge = sb < g.fs0 || sb >= g.fs1;
-    const uint32_t r = (uint32_t)(sb - g.fs0);                                     // superblock of the full range
-    const uint32_t t = (uint32_t)(((uint64_t)(r >> 3) * g.Lmagic) >> 40);          // task = r / W = (r / 8) / L
-    const uint32_t full = g.sb_word + (uint32_t)arena_sb_word(t, r - t * 8 * g.L, gg, g.W);  // wave = r - t W
+    const uint32_t full = g.sb_word + (uint32_t)(sb - g.fs0) * 8 + gg;
     const uint32_t ed = g.edge_word + 128u + (sb == g.sb0 ? 0u : 8u) + gg;
     return edge ? ed : full;
   }
 
   // SB[., 0] word indices of the whole superblocks mid_s .. mid_s + 7 (relative to sb0; the first n used, the
-  // rest 0): one task division, then a wave step per superblock that wraps into the next task at most once
-  // (W >= 8). Whole superblocks between two partial ones are never the arena's edge superblocks.
+  // rest 0). Whole superblocks between two partial ones are never the arena's edge superblocks, and SB is
+  // linear in the superblock, so no edge selects.
   __device__ __forceinline__ void mid_addrs(uint32_t mid_s, uint32_t n, uint32_t (&a)[8]) const {
-    const uint32_t r = (uint32_t)(g.sb0 + mid_s - g.fs0);
-    const uint32_t t = (uint32_t)(((uint64_t)(r >> 3) * g.Lmagic) >> 40);
-    const uint32_t W = (uint32_t)g.W, w = r - t * W;
+    const uint32_t w0 = g.sb_word + (uint32_t)(g.sb0 + mid_s - g.fs0) * 8;
 #pragma unroll
-    for (uint32_t q = 0; q < 8; q++) {
-      const uint32_t wq = w + q;
-      const bool wrap = wq >= W;
-      const uint32_t tq = t + (wrap ? 1u : 0u), wv = wrap ? wq - W : wq;
-      a[q] = q < n ? g.sb_word + ((tq / kSTasks) * W + wv) * 8 * kSTasks + tq % kSTasks : 0u;
-    }
+    for (uint32_t q = 0; q < 8; q++) a[q] = q < n ? w0 + 8 * q : 0u;
   }
 
   // Phase A: descriptor, plan, window and register loads (nothing the line pass writes).

@@ -119,10 +119,6 @@ __device__ __forceinline__ void arena_line_pass(const uint8_t* __restrict__ base
   uint32_t q[kSTasks];
 #pragma unroll
   for (uint32_t i = 0; i < kSTasks; i++) q[i] = 0;
-  // SB of the burst's tasks 2j, 2j + 1 for this lane's block (arena_sb_word); every lane has its block's SB
-  static_assert(kSTasks == 16, "8 lanes x 2 SB words per block and burst");
-  uint32_t sbq0 = 0, sbq1 = 0;
-  const size_t wv = g0 / 8;  // the wave's index in the task's superblock order
   // r = raw CRC of this lane's line (line j of block b, its lane group holding the block's 8 lines in
   // order; block h on lane group gq(h)); returns S for it and (lanes j == 0) SB for its block
   auto arena_scan = [&](uint32_t r, uint32_t& sbv, uint32_t b, auto gq) {
@@ -186,15 +182,11 @@ __device__ __forceinline__ void arena_line_pass(const uint8_t* __restrict__ base
     const uint32_t slot = (uint32_t)t & (kSTasks - 1);
 #pragma unroll
     for (uint32_t i = 0; i < kSTasks; i++) q[i] = slot == i ? x : q[i];
-    sbq0 = slot == 2 * j ? sbv : sbq0;
-    sbq1 = slot == 2 * j + 1 ? sbv : sbq1;
+    if constexpr ((PROBE & 6) == 0) {
+      if (j == 0) ar.SB[(((uint64_t)t * ngroups + g0) / 8) * 8 + blk] = sbv;
+    }
     if (slot == kSTasks - 1 || t + 1 == ntasks) {
       const uint64_t t0 = (uint64_t)t & ~(uint64_t)(kSTasks - 1);
-      if constexpr ((PROBE & 6) == 0) {  // (a partial last burst also stores slots past ntasks: never read)
-        typedef unsigned int v2u32 __attribute__((ext_vector_type(2)));
-        const v2u32 w = {sbq0, sbq1};
-        __builtin_nontemporal_store(w, reinterpret_cast<v2u32*>(ar.SB + arena_sb_word(t0, wv, blk, ar.W) + 2 * j));
-      }
       if constexpr ((PROBE & 1) == 0) {
         v4u32* dst = reinterpret_cast<v4u32*>(ar.S + arena_s_word(t0, gblk, j, ar.W));
 #pragma unroll

@@ -146,8 +146,9 @@ hipError_t launch_bucket_place(const uint64_t* off, const uint32_t* len, size_t 
 // superblock the block-suffix CRC S leaves in bursts of K = kSTasks tasks, K / 4 16-byte stores per lane
 // that each cover 1 KiB contiguously: task t of group g, line a at word
 //   ((((t / K) * W + g / 8) * (K / 4) + (t / 4) % (K / 4)) * 256 + ((g % 8) * 8 + a) * 4 + t % 4.
-// SB (superblock suffix per block) in the same bursts, arena_sb_word below. The (at most two) partial
-// superblocks keep S in S_edge[2][64] and SB in SB_edge[2][8].
+// SB (superblock suffix per block) of full superblock fs0 + i, block g at word i * 8 + g: a 128-byte line
+// holds 4 superblocks of one task (W is a multiple of 4), so no line mixes two tasks' stores. The (at
+// most two) partial superblocks keep S in S_edge[2][64] and SB in SB_edge[2][8].
 #ifndef ANNETY_S_TASKS
 #define ANNETY_S_TASKS 16
 #endif
@@ -155,12 +156,6 @@ constexpr uint32_t kSTasks = ANNETY_S_TASKS;  // tasks per S burst (kSTasks / 4 
 inline __host__ __device__ uint64_t arena_s_word(uint64_t t, uint64_t group, uint32_t a, uint64_t W) {
   return ((((t / kSTasks) * W + (group >> 3)) * (kSTasks / 4) + ((t >> 2) % (kSTasks / 4))) << 8) +
          (((group & 7) * 8 + a) << 2) + (t & 3);
-}
-// SB in the same bursts: a wave's kSTasks SB words per block leave in one 8-byte store per lane (lane j of
-// the group holding block b keeps tasks 2j and 2j + 1), 512 bytes contiguous per wave:
-// [burst][wave][block b][task % kSTasks].
-inline __host__ __device__ uint64_t arena_sb_word(uint64_t t, uint64_t wave, uint32_t b, uint64_t W) {
-  return (((t / kSTasks) * W + wave) * 8 + b) * kSTasks + (t % kSTasks);
 }
 
 // Geometry of one arena call: the line pass on `blocks` workgroups, and the scratch layout
@@ -180,7 +175,7 @@ inline ArenaGeom arena_geom(const ArenaLaunch& a, size_t line_blocks) {  // line
   g.ntasks = (nsbf + g.W - 1) / g.W;
   g.nbursts = (g.ntasks + kSTasks - 1) / kSTasks;
   g.sb_off = g.nbursts * g.W * 64 * kSTasks;
-  g.edge_off = g.sb_off + g.nbursts * g.W * 8 * kSTasks;
+  g.edge_off = g.sb_off + nsbf * 8;
   g.words = g.edge_off + 144;
   return g;
 }
