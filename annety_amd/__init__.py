@@ -25,8 +25,10 @@ from .crc32c import (  # noqa: F401
     PinnedHostBuffer,
     StreamingCrc,
     digests_to_numpy,
+    last_kernels,
     reserve_cus,
     scratch_stats,
+    set_frames_pack,
     set_split,
     set_walk_segment,
     stream_release,
@@ -47,8 +49,10 @@ __all__ = [
     "crc32_batch_host",
     "crc32_combine",
     "digests_to_numpy",
+    "last_kernels",
     "reserve_cus",
     "scratch_stats",
+    "set_frames_pack",
     "set_split",
     "set_walk_segment",
     "stream_release",

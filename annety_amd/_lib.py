@@ -21,6 +21,9 @@ SIGNATURES = [
     ("annety_crc_shutdown", ctypes.c_int, []),
     ("annety_crc_strerror", ctypes.c_char_p, [ctypes.c_int]),
     ("annety_crc_last_hip_error", ctypes.c_int, []),
+    ("annety_crc_last_error_stage", ctypes.c_char_p, []),
+    ("annety_crc_last_kernels", ctypes.c_char_p, []),
+    ("annety_crc_set_frames_pack", ctypes.c_int, [ctypes.c_int]),
     ("annety_crc_reserve_cus", ctypes.c_int, [ctypes.c_int]),
     ("annety_crc_set_split", ctypes.c_int, [ctypes.c_int, _u64]),
     ("annety_crc_set_walk_segment", ctypes.c_int, [_u64]),
@@ -80,8 +83,11 @@ class CrcError(RuntimeError):
         lib = get()
         msg = lib.annety_crc_strerror(status).decode()
         hip = lib.annety_crc_last_hip_error()
-        super().__init__(f"{where}: {msg} (status {status}, hipError {hip})")
+        stage = (lib.annety_crc_last_error_stage() or b"").decode()
+        super().__init__(f"{where}: {msg} (status {status}, hipError {hip}"
+                         + (f", stage: {stage})" if stage and hip else ")"))
         self.status = status
+        self.stage = stage
 
 
 def lib_path() -> str:
@@ -91,10 +97,16 @@ def lib_path() -> str:
 def get() -> ctypes.CDLL:
     global _lib
     if _lib is None:
-        if not os.path.exists(_build.LIB):
+        # ANNETY_CRC_HOST_LIB: a host-only sanitizer build of crc32_host.cpp (annety_amd/csrc/Makefile), for
+        # running the host-side tests (frame walks, encode plans, shard plans) under ASan/UBSan or TSan; it
+        # exports the host entry points only, so the device ones stay unbound and any call to them fails.
+        host_only = os.environ.get("ANNETY_CRC_HOST_LIB")
+        if not host_only and not os.path.exists(_build.LIB):
             _build.build()  # raises if hipcc is unavailable: no silent fallback
-        lib = ctypes.CDLL(_build.LIB)
+        lib = ctypes.CDLL(host_only or _build.LIB)
         for name, res, args in SIGNATURES:
+            if host_only and not hasattr(lib, name):
+                continue
             f = getattr(lib, name)
             f.restype = res
             f.argtypes = args

@@ -86,6 +86,17 @@ def set_walk_segment(nbytes: int = 0) -> None:
     _lib.check(_lib.get().annety_crc_set_walk_segment(int(nbytes)), "annety_crc_set_walk_segment")
 
 
+def set_frames_pack(pack: bool = True) -> None:
+    """annety_crc_set_frames_pack: receive buffers not pinned through PinnedHostBuffer are packed into the
+    library's pinned ring (True, default) or handed to the runtime's pageable copy (False). Process-wide."""
+    _lib.check(_lib.get().annety_crc_set_frames_pack(1 if pack else 0), "annety_crc_set_frames_pack")
+
+
+def last_kernels() -> str:
+    """annety_crc_last_kernels: the kernels this thread's latest device call enqueued, in order."""
+    return (_lib.get().annety_crc_last_kernels() or b"").decode()
+
+
 def set_split(mode: int = -1, min_segment: int = 0) -> None:
     """annety_crc_set_split: long-payload split policy (-1 auto, 0 never, 1 always), process-wide."""
     _lib.check(_lib.get().annety_crc_set_split(int(mode), int(min_segment)), "annety_crc_set_split")
@@ -306,16 +317,32 @@ def crc32_batch_host(buf: BytesLike, n: int, length: int, stride: Optional[int] 
 
 class PinnedHostBuffer:
     """A host buffer registered with the device runtime (annety_crc_host_register), e.g. the arena a
-    NetBuffer reads sockets into: host batches over it are copied to the device in place."""
+    NetBuffer reads sockets into: host batches over it are copied to the device in place.
+
+    The memory is an anonymous mapping of whole pages, so the registration starts on a page boundary and
+    shares no page with any other buffer (the library refuses registrations that would: DESIGN.md 7.3)."""
 
     def __init__(self, nbytes: int):
-        self.array = np.empty(nbytes, dtype=np.uint8)
-        _lib.check(_lib.get().annety_crc_host_register(self.array.ctypes.data, nbytes), "annety_crc_host_register")
+        import mmap
+
+        nbytes = max(1, int(nbytes))
+        pg = mmap.PAGESIZE
+        self._map = mmap.mmap(-1, (nbytes + pg - 1) // pg * pg, flags=mmap.MAP_PRIVATE | mmap.MAP_ANONYMOUS)
+        self._pages = np.frombuffer(self._map, dtype=np.uint8)
+        self.array = self._pages[:nbytes]
+        _lib.check(_lib.get().annety_crc_host_register(self._pages.ctypes.data, self._pages.size),
+                   "annety_crc_host_register")
 
     def close(self):
-        if self.array is not None:
-            _lib.get().annety_crc_host_unregister(self.array.ctypes.data)
-            self.array = None
+        if self.array is None:
+            return
+        _lib.get().annety_crc_host_unregister(self._pages.ctypes.data)
+        self.array = self._pages = None
+        try:
+            self._map.close()  # BufferError while a caller still holds a view: the mapping then goes with it
+        except BufferError:
+            pass
+        self._map = None
 
     def __del__(self):
         try:

@@ -701,6 +701,7 @@ hipError_t launch_extent(const uint64_t* off, const uint32_t* len, size_t n, voi
                          const BucketArgs* bk, hipStream_t stream) {
   const unsigned blocks = bucket_grid(n);
   *parts = blocks;
+  note_kernel(bk ? "crc32_extent_kernel<count>" : "crc32_extent_kernel");
   if (bk)
     hipLaunchKernelGGL(crc32_extent_kernel<true>, dim3(blocks), dim3(kExtentBlock), 0, stream, off, len, n,
                        static_cast<uint64_t*>(ws), *bk);
@@ -712,6 +713,7 @@ hipError_t launch_extent(const uint64_t* off, const uint32_t* len, size_t n, voi
 
 hipError_t launch_bucket_place(const uint64_t* off, const uint32_t* len, size_t n, const void* ws, uint32_t parts,
                                const BucketArgs& bk, ExtentHint* record, uint64_t seq, hipStream_t stream) {
+  note_kernel("crc32_bucket_place");
   hipLaunchKernelGGL(crc32_bucket_place, dim3(bucket_grid(n)), dim3(kBucketThreads), 0, stream, off, len, n,
                      static_cast<const uint64_t*>(ws), parts, bk, record, seq);
   return hipGetLastError();
@@ -784,6 +786,7 @@ hipError_t launch_stitch_p(const ArenaLaunch& a, hipStream_t stream) {
   const size_t blocks = stitch_blocks(a, BLK);
   const uint4* img_slice = static_cast<const uint4*>(a.img_slice);
   const uint4* img_stitch = static_cast<const uint4*>(a.img_stitch);
+  note_kernel("crc32_arena_stitch_kernel");
   if (a.update)
     hipLaunchKernelGGL((crc32_arena_stitch_kernel<true, BLK, PROBE, PIPE>), dim3((unsigned)blocks), dim3(BLK), 0,
                        stream, s, img_slice, img_stitch);
@@ -810,6 +813,7 @@ template <int PROBE, bool NT = true>
 hipError_t launch_arena_lines_p(const ArenaLaunch& a, hipStream_t stream) {
   static_assert(kBlock / 8 == 64 && kSTasks % 4 == 0, "arena_geom / arena_s_word assume 64 groups per block, bursts of 4k tasks");
   const ArenaGeom geo = arena_geom(a);
+  note_kernel("crc32_arena_lines_kernel");
   hipLaunchKernelGGL((crc32_arena_lines_kernel<PROBE, NT>), dim3((unsigned)geo.blocks), dim3(kBlock), 0, stream,
                      reinterpret_cast<const uint8_t*>((uintptr_t)(a.fs0 * 8192)), line_out(a, geo), static_cast<const uint4*>(a.img_slice), static_cast<const uint4*>(a.img_group8),
                      static_cast<const uint4*>(a.img_sb));

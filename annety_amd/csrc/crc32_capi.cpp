@@ -8,25 +8,51 @@
 #include <algorithm>
 #include <atomic>
 #include <cstdlib>
-#include <condition_variable>
 #include <cstring>
-#include <functional>
 #include <memory>
 #include <mutex>
+#include <string>
 #include <thread>
 #include <vector>
 
+#include "crc32_host.h"
 #include "crc32_kernels.h"
 #include "crc32_math.h"
 
 using namespace annety_crc;
+using host::ConnWalk;
+using host::FrameRules;
+using host::FrameWalks;
+using host::kPbcRules;
+using host::lhc_rules;
+using host::lhc_type_ok;
+using host::parallel_pack;
 
 namespace {
 
+// ---------------- error and launch records (per calling thread) ----------------
 thread_local int t_last_hip = 0;
+// The stage a host path is in (verify_host_iov names its steps), and the stage of the last failing HIP call:
+// annety_crc_last_error_stage. A failure of queued work surfaces at the next synchronising call, so with
+// ANNETY_CRC_SYNC_STAGES=1 the host paths synchronise after every stage to name the one that failed.
+thread_local const char* t_stage = "";
+thread_local const char* t_fail_stage = "";
+// The kernels the latest device entry point of this thread launched, in order (annety_crc_last_kernels).
+thread_local std::string t_kernels;
+
+void set_stage(const char* s) { t_stage = s; }
+
+bool sync_stages() {
+  static const bool on = [] {
+    const char* e = std::getenv("ANNETY_CRC_SYNC_STAGES");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
 
 int hip_fail(hipError_t e) {
   t_last_hip = static_cast<int>(e);
+  t_fail_stage = t_stage;
   return e == hipErrorOutOfMemory ? ANNETY_CRC_ENOMEM : ANNETY_CRC_EHIP;
 }
 
@@ -36,164 +62,10 @@ int hip_fail(hipError_t e) {
     if (e_ != hipSuccess) return hip_fail(e_); \
   } while (0)
 
-// ---------------- host worker pools (staging packs, frame walks) ----------------
-// Pageable -> pinned packing is a host memcpy; one thread moves ~10-20 GB/s, below PCIe Gen5 x16, so the
-// pack is split over a small persistent pool (ANNETY_CRC_PACK_THREADS, default min(8, cores)). Several
-// callers may pack at once (the device group's per-device threads, concurrent host batches): each run() is
-// a job in a shared list, the workers take pieces of any job, and every caller also works on its own job
-// until it is done, so concurrent packs share the workers instead of queueing behind one another.
-// The frame walks (FrameWalks) use a second pool the same way, started with submit() so that they run
-// while the caller packs; persistent threads, because creating eight threads per call cost milliseconds
-// in a process with a busy address space.
-class WorkPool {
- public:
-  struct Job {
-    std::function<void(size_t)> fn;
-    size_t next = 0, total = 0, left = 0;
-    std::condition_variable done_cv;
-  };
-  WorkPool(int workers) {
-    for (int i = 0; i < workers; i++) workers_.emplace_back([this] { loop(); });
-  }
-  ~WorkPool() {
-    {
-      std::lock_guard<std::mutex> lk(mu_);
-      stop_ = true;
-    }
-    cv_.notify_all();
-    for (auto& w : workers_) w.join();
-  }
-  int threads() const { return (int)workers_.size() + 1; }
-  // Queues fn(i) for i in [0, n) to the workers; wait() on the returned job.
-  std::unique_ptr<Job> submit(size_t n, std::function<void(size_t)> fn) {
-    auto job = std::make_unique<Job>();
-    job->fn = std::move(fn);
-    job->total = job->left = n;
-    if (n) {
-      {
-        std::lock_guard<std::mutex> lk(mu_);
-        jobs_.push_back(job.get());
-      }
-      cv_.notify_all();
-    }
-    return job;
-  }
-  // The caller works on what is left of the job, then waits until the workers' pieces are done.
-  void wait(Job& job) {
-    for (;;) {
-      size_t i;
-      {
-        std::lock_guard<std::mutex> lk(mu_);
-        if (job.next >= job.total) break;
-        i = job.next++;
-      }
-      job.fn(i);
-      finish(job);
-    }
-    std::unique_lock<std::mutex> lk(mu_);
-    job.done_cv.wait(lk, [&] { return job.left == 0; });
-    const auto it = std::find(jobs_.begin(), jobs_.end(), &job);
-    if (it != jobs_.end()) jobs_.erase(it);
-  }
-  // Runs fn(i) for i in [0, n) on the pool and the calling thread; returns when all are done.
-  template <class F>
-  void run(size_t n, F&& fn) {
-    if (n == 0) return;
-    if (workers_.empty() || n == 1) {
-      for (size_t i = 0; i < n; i++) fn(i);
-      return;
-    }
-    auto job = submit(n, std::function<void(size_t)>(std::ref(fn)));
-    wait(*job);
-  }
-
- private:
-  void finish(Job& job) {
-    std::lock_guard<std::mutex> lk(mu_);
-    if (--job.left == 0) job.done_cv.notify_all();
-  }
-  void loop() {
-    for (;;) {
-      Job* job = nullptr;
-      size_t i = 0;
-      {
-        std::unique_lock<std::mutex> lk(mu_);
-        cv_.wait(lk, [&] {
-          if (stop_) return true;
-          for (Job* j : jobs_)
-            if (j->next < j->total) return true;
-          return false;
-        });
-        if (stop_) return;
-        for (Job* j : jobs_)
-          if (j->next < j->total) {
-            job = j;
-            break;
-          }
-        i = job->next++;
-      }
-      job->fn(i);
-      finish(*job);
-    }
-  }
-  std::vector<std::thread> workers_;
-  std::mutex mu_;
-  std::condition_variable cv_;
-  std::vector<Job*> jobs_;  // jobs with pieces left or still being finished (owned by their callers)
-  bool stop_ = false;
-};
-
-int pool_threads(const char* env, int dflt) {
-  int t = dflt;
-  if (const char* e = std::getenv(env)) t = std::max(1, std::min(64, std::atoi(e)));
-  return t;
-}
-WorkPool& pack_pool() {  // the caller is one of the threads
-  static WorkPool pool(pool_threads("ANNETY_CRC_PACK_THREADS",
-                                    (int)std::min<unsigned>(8, std::max<unsigned>(1, std::thread::hardware_concurrency()))) -
-                       1);
-  return pool;
-}
-WorkPool& walk_pool() {  // submitted jobs run on the workers alone until the caller waits
-  static WorkPool pool(pool_threads("ANNETY_CRC_WALK_THREADS",
-                                    (int)std::min<unsigned>(8, std::max<unsigned>(1, std::thread::hardware_concurrency()))));
-  return pool;
-}
-
-// dst[i*dstride, +len) = src[i*sstride, +len) for i < cnt, in parallel pieces of >= 1 MiB.
-void parallel_pack(char* dst, size_t dstride, const char* src, size_t sstride, size_t cnt, size_t len) {
-  if (dstride == sstride && dstride == len) {  // one contiguous block
-    const size_t bytes = cnt * len, piece = std::max<size_t>(1 << 20, bytes / (4 * pack_pool().threads()) + 1);
-    pack_pool().run((bytes + piece - 1) / piece, [&](size_t i) {
-      const size_t lo = i * piece, hi = std::min(bytes, lo + piece);
-      std::memcpy(dst + lo, src + lo, hi - lo);
-    });
-    return;
-  }
-  const size_t per = std::max<size_t>(1, (1 << 20) / std::max<size_t>(len, 1));
-  pack_pool().run((cnt + per - 1) / per, [&](size_t i) {
-    const size_t lo = i * per, hi = std::min(cnt, lo + per);
-    for (size_t k = lo; k < hi; k++) std::memcpy(dst + k * dstride, src + k * sstride, len);
-  });
-}
-
-// true if [p, p + bytes) is pinned (hipHostMalloc'd or hipHostRegister'ed) host memory, so the DMA
-// engines can read it in place.
-bool host_pinned(const void* p, size_t bytes) {
-  hipPointerAttribute_t at{};
-  if (hipPointerGetAttributes(&at, p) != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
-  if (at.type != hipMemoryTypeHost) return false;
-  if (bytes <= 1) return true;
-  hipPointerAttribute_t end{};
-  if (hipPointerGetAttributes(&end, static_cast<const char*>(p) + bytes - 1) != hipSuccess) {
-    (void)hipGetLastError();
-    return false;
-  }
-  return end.type == hipMemoryTypeHost;
-}
+// true if [p, p + bytes) lies inside one range this library pinned (annety_crc_host_register), so the DMA
+// engines can read it in place. The runtime's pointer attributes are not asked: they classify a range by
+// single bytes and cannot tell a stale or partly overlapping registration from a live one.
+bool host_pinned(const void* p, size_t bytes) { return host::host_registry().covers(p, bytes); }
 
 // ---------------- host-built LDS images ----------------
 constexpr int kGroups[] = {1, 2, 4, 8, 16, 32};
@@ -359,6 +231,67 @@ struct Staging {
   size_t h_meta_cap = 0;   // frames
 };
 
+// The scratch a stream's slot carries (crc32_host.h Slot<Scratch>::data).
+struct Scratch {
+  void* ptr = nullptr;
+  size_t bytes = 0;
+  // automatic variable-path choice (run_var_auto): the extent kernels' area is the slot's first
+  // kExtentScratchBytes; the paths' scratch follows
+  ExtentHint* hint = nullptr;  // pinned: the extent of this slot's latest completed auto call
+  uint64_t calls = 0;          // extent kernels launched from this slot (hint->seq numbers them)
+  // the sorted path's bucket cursors (crc32_kernels.h BucketArgs): set (sorts & 1) is this call's
+  uint64_t sorts = 0;
+  bool cursors_clean = false;  // both sets zero (false after an allocation or a failed sort)
+  struct Key {
+    const void *base, *off, *len;
+    size_t n;
+    bool update;
+    bool operator==(const Key& o) const {
+      return base == o.base && off == o.off && len == o.len && n == o.n && update == o.update;
+    }
+  } key{};
+  uint64_t key_since = 0;                 // first call (seq) with the current key
+  uint64_t since_extent = 0;              // arena calls since the last one that recorded its extent
+  uint64_t seen_seq = 0, prev_seq = 0;    // the two latest completed hints read for this key
+  ExtentHint seen{}, prev{};
+};
+using ScratchSlot = host::Slot<Scratch>;
+
+// Up to ANNETY_CRC_STREAM_SLOTS (default 64) slots per device, read once.
+size_t stream_slot_cap() {
+  static const size_t cap = [] {
+    const char* e = std::getenv("ANNETY_CRC_STREAM_SLOTS");
+    const long v = e && *e ? std::atol(e) : 64;
+    return (size_t)std::max(1L, std::min(4096L, v));
+  }();
+  return cap;
+}
+
+// The runtime operations the slot table needs, on the current device.
+struct HipSlotOps {
+  int make_fence(void** ev) {
+    hipEvent_t e = nullptr;
+    HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    *ev = e;
+    return ANNETY_CRC_OK;
+  }
+  void destroy_fence(void* ev) {
+    if (ev) (void)hipEventDestroy(static_cast<hipEvent_t>(ev));
+  }
+  int record(void* ev, const void* stream) {
+    HIP_TRY(hipEventRecord(static_cast<hipEvent_t>(ev), static_cast<hipStream_t>(const_cast<void*>(stream))));
+    return ANNETY_CRC_OK;
+  }
+  int wait(const void* stream, void* ev) {
+    HIP_TRY(hipStreamWaitEvent(static_cast<hipStream_t>(const_cast<void*>(stream)), static_cast<hipEvent_t>(ev), 0));
+    return ANNETY_CRC_OK;
+  }
+  int drain() {
+    HIP_TRY(hipDeviceSynchronize());
+    return ANNETY_CRC_OK;
+  }
+};
+
 struct DeviceCtx {
   std::atomic<bool> ready{false};
   int cus = 0;
@@ -372,41 +305,12 @@ struct DeviceCtx {
   std::mutex stg_mu;  // one host-staged batch at a time per device
   std::mutex pow_mu;  // split-path power tables, one per segment size
   std::vector<std::pair<uint64_t, uint32_t*>> powers;
-  // per-call scratch of the arena, split and sorted paths, reused across calls: one slot per stream,
-  // fenced by stream order (scratch_slot)
-  struct ScratchSlot {
-    void* ptr = nullptr;
-    size_t bytes = 0;
-    hipStream_t last = nullptr;  // the stream of the last call that used the slot
-    std::thread::id tid{};       // last == hipStreamPerThread: the thread the handle resolved to
-    uint64_t tick = 0;           // last use, for LRU hand-over
-    hipEvent_t fence = nullptr;  // recorded on `last` only when the slot is handed to another stream
-                                 // (per-thread handles: after every call, see scratch_done)
-    // automatic variable-path choice (run_var_auto): the extent kernels' area is the slot's first
-    // kExtentScratchBytes; the paths' scratch follows
-    ExtentHint* hint = nullptr;  // pinned: the extent of this slot's latest completed auto call
-    uint64_t calls = 0;          // extent kernels launched from this slot (hint->seq numbers them)
-    // the sorted path's bucket cursors (crc32_kernels.h BucketArgs): set (sorts & 1) is this call's
-    uint64_t sorts = 0;
-    bool cursors_clean = false;  // both sets zero (false after an allocation or a failed sort)
-    struct Key {
-      const void *base, *off, *len;
-      size_t n;
-      bool update;
-      bool operator==(const Key& o) const {
-        return base == o.base && off == o.off && len == o.len && n == o.n && update == o.update;
-      }
-    } key{};
-    uint64_t key_since = 0;                 // first call (seq) with the current key
-    uint64_t since_extent = 0;              // arena calls since the last one that recorded its extent
-    uint64_t seen_seq = 0, prev_seq = 0;    // the two latest completed hints read for this key
-    ExtentHint seen{}, prev{};
-  };
+  // per-call scratch of the arena, split and sorted paths, reused across calls: one slot per stream
+  // (crc32_host.h SlotTable: stream order while the table has room, fences or one drain past it)
   std::mutex arena_mu;  // held while a call picks a slot and enqueues its launches
-  std::vector<std::unique_ptr<ScratchSlot>> slots;
-  uint64_t tick = 0;
-  // test-visible counters (annety_crc_scratch_stats)
-  std::atomic<uint64_t> handoffs{0}, device_syncs{0};
+  host::SlotTable<Scratch> slots{stream_slot_cap()};
+  // test-visible counters (annety_crc_scratch_stats): drains at shutdown (the table counts its own)
+  std::atomic<uint64_t> shutdown_syncs{0};
   std::atomic<uint64_t> auto_arena{0}, auto_sorted{0};  // run_var_auto's choices
   std::atomic<uint64_t> auto_unchecked{0};              // arena calls without the extent kernel
 };
@@ -486,6 +390,8 @@ DeviceCtx* ensure_ctx(int dev, int* rc) {
 bool special_stream(hipStream_t s) { return s == nullptr || s == hipStreamPerThread || s == hipStreamLegacy; }
 
 int stream_ctx(hipStream_t stream, DeviceCtx** out) {
+  t_kernels.clear();  // a device entry point starts: its launches are recorded from here
+  set_stage("launch");
   int dev = 0;
   HIP_TRY(hipGetDevice(&dev));
   if (!special_stream(stream)) {
@@ -568,76 +474,35 @@ int run_var(DeviceCtx& c, const void* d_base, size_t n, uint64_t fstride, uint32
   return ANNETY_CRC_OK;
 }
 
-// Per-call device scratch of the arena, split and sorted paths, one slot per stream, reused in stream
-// order with no per-call event (recording one after each call cost 2-4 us of GPU time per call: config 3
-// 0.2111-0.2173 vs 0.2068-0.2089 ms per step, profiles/r02/arena_events_ab/; the stream-ordered allocator
-// per call cost ~3.6 us). Slots are keyed by stream handle, and for hipStreamPerThread also by calling
-// thread (that one handle names a different stream in every thread). Up to stream_slot_cap() slots per
-// device (ANNETY_CRC_STREAM_SLOTS, default 64); past that the least recently used slot is handed over:
-// an event recorded on its last stream at that moment, waited by the new stream (hipStreamWaitEvent), so
-// no host thread and no other stream ever waits for the hand-over. The caller holds c.arena_mu from here
-// until its launches are enqueued, then calls scratch_done.
-size_t stream_slot_cap() {
-  static const size_t cap = [] {
-    const char* e = std::getenv("ANNETY_CRC_STREAM_SLOTS");
-    const long v = e && *e ? std::atol(e) : 64;
-    return (size_t)std::max(1L, std::min(4096L, v));
-  }();
-  return cap;
-}
-
-bool same_owner(const DeviceCtx::ScratchSlot& s, hipStream_t stream) {
-  return s.last == stream && (stream != hipStreamPerThread || s.tid == std::this_thread::get_id());
-}
-
-int scratch_slot(DeviceCtx& c, hipStream_t stream, size_t bytes, DeviceCtx::ScratchSlot** out) {
-  DeviceCtx::ScratchSlot* slot = nullptr;
-  for (auto& s : c.slots)
-    if (same_owner(*s, stream)) {
-      slot = s.get();
-      break;
-    }
-  if (!slot && c.slots.size() < stream_slot_cap()) {
-    auto fresh = std::make_unique<DeviceCtx::ScratchSlot>();
-    HIP_TRY(hipEventCreateWithFlags(&fresh->fence, hipEventDisableTiming));
-    slot = fresh.get();
-    c.slots.push_back(std::move(fresh));
-  } else if (!slot) {
-    // hand the least recently used slot over: the new stream waits for everything its last stream had
-    // queued so far (which includes that stream's last use of the slot)
-    slot = c.slots.front().get();
-    for (auto& s : c.slots)
-      if (s->tick < slot->tick) slot = s.get();
-    if (slot->last != hipStreamPerThread) HIP_TRY(hipEventRecord(slot->fence, slot->last));
-    // a per-thread slot's fence was recorded by its own thread after its last call (scratch_done)
-    HIP_TRY(hipStreamWaitEvent(stream, slot->fence, 0));
-    c.handoffs++;
+// Per-call device scratch of the arena, split and sorted paths: the stream's slot (crc32_host.h SlotTable),
+// grown in stream order with the stream-ordered allocator (one allocation per growth; per call it would cost
+// ~3.6 us). The caller holds c.arena_mu from here until its launches are enqueued, then calls scratch_done.
+int scratch_slot(DeviceCtx& c, hipStream_t stream, size_t bytes, ScratchSlot** out) {
+  HipSlotOps ops;
+  ScratchSlot* slot = nullptr;
+  const int rc = c.slots.acquire(ops, stream, stream == hipStreamPerThread, &slot);
+  if (rc) return rc;
+  Scratch& d = slot->data;
+  if (d.bytes < bytes) {
+    if (d.ptr) HIP_TRY(hipFreeAsync(d.ptr, stream));
+    d.ptr = nullptr;
+    d.bytes = 0;
+    HIP_TRY(hipMallocAsync(&d.ptr, kExtentScratchBytes + bytes, stream));
+    d.bytes = bytes;
+    d.cursors_clean = false;
   }
-  if (slot->bytes < bytes) {
-    if (slot->ptr) HIP_TRY(hipFreeAsync(slot->ptr, stream));
-    slot->ptr = nullptr;
-    slot->bytes = 0;
-    HIP_TRY(hipMallocAsync(&slot->ptr, kExtentScratchBytes + bytes, stream));
-    slot->bytes = bytes;
-    slot->cursors_clean = false;
-  }
-  slot->last = stream;
-  slot->tid = std::this_thread::get_id();
-  slot->tick = ++c.tick;
   *out = slot;
   return ANNETY_CRC_OK;
 }
 
 // The paths' scratch inside a slot (after the extent kernel's area).
-char* path_scratch(const DeviceCtx::ScratchSlot* slot) { return static_cast<char*>(slot->ptr) + kExtentScratchBytes; }
+char* path_scratch(const ScratchSlot* slot) { return static_cast<char*>(slot->data.ptr) + kExtentScratchBytes; }
 
-// After the call's launches on `stream` (arena_mu still held). hipStreamPerThread resolves to the calling
-// thread's stream, which no other thread can name when it takes the slot over: such slots record their
-// fence after every call (the 2-4 us marker, paid only by callers that use the per-thread handle).
-int scratch_done(DeviceCtx::ScratchSlot* slot, hipStream_t stream) {
-  if (stream != hipStreamPerThread) return ANNETY_CRC_OK;
-  const hipError_t r = hipEventRecord(slot->fence, stream);
-  return r == hipSuccess ? ANNETY_CRC_OK : hip_fail(r);
+// After the call's launches (arena_mu still held): the table fences the call when a later hand-over could
+// need it (crc32_host.h SlotTable::done).
+int scratch_done(DeviceCtx& c, ScratchSlot* slot) {
+  HipSlotOps ops;
+  return c.slots.done(ops, slot);
 }
 
 // Variable batch: counting sort by line count on the device (no host round trip; two launches,
@@ -660,14 +525,14 @@ bool sorted_fused() {
 
 // The sorted path's launches into `slot` (sized by sorted_scratch_bytes; c.arena_mu held). `record`
 // (automatic path): the extent record the bucket pass publishes, numbered `seq`.
-int run_var_sorted_in(DeviceCtx& c, DeviceCtx::ScratchSlot* slot, const void* d_base, size_t n, const uint64_t* d_off,
+int run_var_sorted_in(DeviceCtx& c, ScratchSlot* slot, const void* d_base, size_t n, const uint64_t* d_off,
                       const uint32_t* d_len, uint32_t* d_out, hipStream_t stream, bool update,
                       ExtentHint* record = nullptr, uint64_t seq = 0) {
-  uint32_t* cursors = reinterpret_cast<uint32_t*>(static_cast<char*>(slot->ptr) + kCursorOff);
-  if (!slot->cursors_clean) {
+  uint32_t* cursors = reinterpret_cast<uint32_t*>(static_cast<char*>(slot->data.ptr) + kCursorOff);
+  if (!slot->data.cursors_clean) {
     const hipError_t z = hipMemsetAsync(cursors, 0, 2 * kBucketCount * sizeof(uint32_t), stream);
     if (z != hipSuccess) return hip_fail(z);
-    slot->cursors_clean = true;
+    slot->data.cursors_clean = true;
   }
   const size_t rows_words = (size_t)bucket_grid(n) * kBucketCount;
   char* scratch = path_scratch(slot);
@@ -676,18 +541,18 @@ int run_var_sorted_in(DeviceCtx& c, DeviceCtx::ScratchSlot* slot, const void* d_
   bk.rows = reinterpret_cast<uint32_t*>(scratch);
   bk.ranges = bk.rows + rows_words;
   bk.desc = scratch + (rows_words + 8) * sizeof(uint32_t);
-  const uint32_t set = (uint32_t)(slot->sorts & 1);
+  const uint32_t set = (uint32_t)(slot->data.sorts & 1);
   bk.cursor = cursors + set * kBucketCount;
   bk.cursor_next = cursors + (set ^ 1) * kBucketCount;
   bk.out = update ? nullptr : d_out;
   uint32_t parts = 0;
-  hipError_t e = launch_extent(d_off, d_len, n, slot->ptr, &parts, &bk, stream);
-  if (e == hipSuccess) e = launch_bucket_place(d_off, d_len, n, slot->ptr, parts, bk, record, seq, stream);
+  hipError_t e = launch_extent(d_off, d_len, n, slot->data.ptr, &parts, &bk, stream);
+  if (e == hipSuccess) e = launch_bucket_place(d_off, d_len, n, slot->data.ptr, parts, bk, record, seq, stream);
   if (e != hipSuccess) {
-    slot->cursors_clean = false;  // the next sort zeroes both sets first
+    slot->data.cursors_clean = false;  // the next sort zeroes both sets first
     return hip_fail(e);
   }
-  slot->sorts++;
+  slot->data.sorts++;
   int rc = ANNETY_CRC_OK;
   if (sorted_fused()) {  // the three length classes in one launch (crc32_var_sorted_kernel)
     VarLaunch a{};
@@ -712,11 +577,11 @@ int run_var_sorted_in(DeviceCtx& c, DeviceCtx::ScratchSlot* slot, const void* d_
 int run_var_sorted(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_off, const uint32_t* d_len,
                    uint32_t* d_out, hipStream_t stream, bool update = false) {
   std::lock_guard<std::mutex> lk(c.arena_mu);
-  DeviceCtx::ScratchSlot* slot = nullptr;
+  ScratchSlot* slot = nullptr;
   int rc = scratch_slot(c, stream, sorted_scratch_bytes(n), &slot);
   if (rc) return rc;
   rc = run_var_sorted_in(c, slot, d_base, n, d_off, d_len, d_out, stream, update);
-  const int rd = scratch_done(slot, stream);
+  const int rd = scratch_done(c, slot);
   return rc ? rc : rd;
 }
 
@@ -766,12 +631,12 @@ int run_arena(DeviceCtx& c, const void* d_base, size_t arena_bytes, const uint64
   const size_t bytes = arena_geom(a).words * sizeof(uint32_t);
   if (bytes / sizeof(uint32_t) >= (1ull << 32)) return ANNETY_CRC_EINVAL;  // the stitch's 32-bit word indices
   std::lock_guard<std::mutex> lk(c.arena_mu);
-  DeviceCtx::ScratchSlot* slot = nullptr;
+  ScratchSlot* slot = nullptr;
   const int rc = scratch_slot(c, stream, bytes, &slot);
   if (rc) return rc;
   a.scratch = reinterpret_cast<uint32_t*>(path_scratch(slot));
   const hipError_t e = launch_arena(a, stream);
-  const int rd = scratch_done(slot, stream);
+  const int rd = scratch_done(c, slot);
   if (e != hipSuccess) return hip_fail(e);
   return rd;
 }
@@ -813,7 +678,8 @@ bool range_mapped(uint64_t lo, uint64_t hi) {
 }
 
 // Reads the slot's pinned record; true if a new completed one for the current key arrived.
-bool poll_hint(DeviceCtx::ScratchSlot* s) {
+bool poll_hint(ScratchSlot* slot) {
+  Scratch* s = &slot->data;
   ExtentHint h{};
   h.lo = __atomic_load_n(&s->hint->lo, __ATOMIC_RELAXED);
   h.hi = __atomic_load_n(&s->hint->hi, __ATOMIC_RELAXED);
@@ -837,24 +703,24 @@ int run_var_auto(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_o
                  uint32_t* d_out, hipStream_t stream, bool update) {
   if (!var_auto() || n < kAutoMinPayloads) return run_var_sorted(c, d_base, n, d_off, d_len, d_out, stream, update);
   std::lock_guard<std::mutex> lk(c.arena_mu);
-  DeviceCtx::ScratchSlot* slot = nullptr;
+  ScratchSlot* slot = nullptr;
   int rc = scratch_slot(c, stream, sorted_scratch_bytes(n), &slot);
   if (rc) return rc;
-  if (!slot->hint) {
-    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&slot->hint), sizeof(ExtentHint), hipHostMallocCoherent | hipHostMallocMapped));
-    std::memset(slot->hint, 0, sizeof(ExtentHint));
+  if (!slot->data.hint) {
+    HIP_TRY(hipHostMalloc(reinterpret_cast<void**>(&slot->data.hint), sizeof(ExtentHint), hipHostMallocCoherent | hipHostMallocMapped));
+    std::memset(slot->data.hint, 0, sizeof(ExtentHint));
   }
-  const DeviceCtx::ScratchSlot::Key key{d_base, d_off, d_len, n, update};
-  if (!(key == slot->key)) {
-    slot->key = key;
-    slot->key_since = slot->calls + 1;
-    slot->seen_seq = slot->prev_seq = 0;
-    slot->since_extent = 0;
+  const Scratch::Key key{d_base, d_off, d_len, n, update};
+  if (!(key == slot->data.key)) {
+    slot->data.key = key;
+    slot->data.key_since = slot->data.calls + 1;
+    slot->data.seen_seq = slot->data.prev_seq = 0;
+    slot->data.since_extent = 0;
   }
   poll_hint(slot);
-  const ExtentHint& h = slot->seen;
-  const bool arena = slot->seen_seq >= slot->key_since && slot->prev_seq >= slot->key_since && !h.bad &&
-                     h.hi > h.lo && h.lo == slot->prev.lo && h.hi == slot->prev.hi && !slot->prev.bad &&
+  const ExtentHint& h = slot->data.seen;
+  const bool arena = slot->data.seen_seq >= slot->data.key_since && slot->data.prev_seq >= slot->data.key_since && !h.bad &&
+                     h.hi > h.lo && h.lo == slot->data.prev.lo && h.hi == slot->data.prev.hi && !slot->data.prev.bad &&
                      h.sum * 3 >= (h.hi - h.lo) * 2 && h.hi - h.lo < (32ull << 30);
   ArenaLaunch a{};
   if (arena) {
@@ -868,38 +734,38 @@ int run_var_auto(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_o
     a.check_lo = h.lo;
     a.check_hi = h.hi;
     if (a.nsb && (rc = scratch_slot(c, stream, arena_geom(a).words * sizeof(uint32_t), &slot))) return rc;
-    if (++slot->since_extent < kAutoRefresh && range_mapped(b + h.lo, b + h.hi)) {
+    if (++slot->data.since_extent < kAutoRefresh && range_mapped(b + h.lo, b + h.hi)) {
       // between two recording calls: the arena launches alone (kAutoRefresh above)
       c.auto_arena++;
       c.auto_unchecked++;
       a.scratch = reinterpret_cast<uint32_t*>(path_scratch(slot));
       const hipError_t e = launch_arena(a, stream);
       rc = e == hipSuccess ? ANNETY_CRC_OK : hip_fail(e);
-      const int rd = scratch_done(slot, stream);
+      const int rd = scratch_done(c, slot);
       return rc ? rc : rd;
     }
-    slot->since_extent = 0;
+    slot->data.since_extent = 0;
   }
   // this call's extent: the check the arena launches make, and the next calls' record (on the sorted
   // path the bucket count runs in the same launch, and the bucket place publishes the record)
-  const uint64_t seq = ++slot->calls;
+  const uint64_t seq = ++slot->data.calls;
   (arena ? c.auto_arena : c.auto_sorted)++;
   if (arena) {
     uint32_t parts = 0;
-    hipError_t e = launch_extent(d_off, d_len, n, slot->ptr, &parts, nullptr, stream);
+    hipError_t e = launch_extent(d_off, d_len, n, slot->data.ptr, &parts, nullptr, stream);
     if (e == hipSuccess) {
-      a.check = static_cast<const uint64_t*>(slot->ptr);
+      a.check = static_cast<const uint64_t*>(slot->data.ptr);
       a.check_parts = parts;
-      a.record = slot->hint;
+      a.record = slot->data.hint;
       a.record_seq = seq;
       a.scratch = reinterpret_cast<uint32_t*>(path_scratch(slot));
       e = launch_arena(a, stream);
     }
     rc = e == hipSuccess ? ANNETY_CRC_OK : hip_fail(e);
   } else {
-    rc = run_var_sorted_in(c, slot, d_base, n, d_off, d_len, d_out, stream, update, slot->hint, seq);
+    rc = run_var_sorted_in(c, slot, d_base, n, d_off, d_len, d_out, stream, update, slot->data.hint, seq);
   }
-  const int rd = scratch_done(slot, stream);
+  const int rd = scratch_done(c, slot);
   return rc ? rc : rd;
 }
 
@@ -980,7 +846,7 @@ int run_split(DeviceCtx& c, const void* d_base, size_t n, uint64_t len, uint64_t
   if (rc) return rc;
   const size_t crc_bytes = (tasks * 4 + 15) & ~(size_t)15;
   std::lock_guard<std::mutex> lk(c.arena_mu);
-  DeviceCtx::ScratchSlot* slot = nullptr;
+  ScratchSlot* slot = nullptr;
   if ((rc = scratch_slot(c, stream, 16 + crc_bytes + 16 * tasks, &slot))) return rc;
   char* scratch = path_scratch(slot);
   uint32_t* range = reinterpret_cast<uint32_t*>(scratch);
@@ -997,32 +863,21 @@ int run_split(DeviceCtx& c, const void* d_base, size_t n, uint64_t len, uint64_t
     hipError_t e = launch_split_join(seg_crc, n, S, powers, d_out, stream);
     if (e != hipSuccess) rc = hip_fail(e);
   }
-  const int rd = scratch_done(slot, stream);
+  const int rd = scratch_done(c, slot);
   return rc ? rc : rd;
 }
 
 }  // namespace
 
-// ---------------- host scalar replacements (drop-in for include/Crc32c.h) ----------------
-namespace annety {
-namespace internal {
-// src/Crc32c.cc:20-92 — same symbols, same contents, generated from the polynomial at compile time.
-#define ANNETY_T256(i) annety_crc::table256_entry(i)
-#define ANNETY_R4(b) ANNETY_T256(b), ANNETY_T256(b + 1), ANNETY_T256(b + 2), ANNETY_T256(b + 3)
-#define ANNETY_R16(b) ANNETY_R4(b), ANNETY_R4(b + 4), ANNETY_R4(b + 8), ANNETY_R4(b + 12)
-#define ANNETY_R64(b) ANNETY_R16(b), ANNETY_R16(b + 16), ANNETY_R16(b + 32), ANNETY_R16(b + 48)
-uint32_t crc32_table256[256] = {ANNETY_R64(0u), ANNETY_R64(64u), ANNETY_R64(128u), ANNETY_R64(192u)};
-#define ANNETY_T16(i) annety_crc::table256_entry(16u * (i))
-uint32_t crc32_table16[16] = {ANNETY_T16(0u),  ANNETY_T16(1u),  ANNETY_T16(2u),  ANNETY_T16(3u),
-                              ANNETY_T16(4u),  ANNETY_T16(5u),  ANNETY_T16(6u),  ANNETY_T16(7u),
-                              ANNETY_T16(8u),  ANNETY_T16(9u),  ANNETY_T16(10u), ANNETY_T16(11u),
-                              ANNETY_T16(12u), ANNETY_T16(13u), ANNETY_T16(14u), ANNETY_T16(15u)};
-}  // namespace internal
-}  // namespace annety
+// crc32_kernels.h: each launcher names the kernel it enqueues (consecutive repeats are kept once).
+void annety_crc::note_kernel(const char* name) {
+  const size_t n = std::strlen(name);
+  if (t_kernels.size() >= n && t_kernels.compare(t_kernels.size() - n, n, name) == 0) return;
+  if (!t_kernels.empty()) t_kernels += " + ";
+  t_kernels += name;
+}
 
 extern "C" {
-
-int annety_crc_abi_version(void) { return ANNETY_CRC_ABI_VERSION; }
 
 int annety_crc_init(int device) {
   if (device < 0 || device >= kMaxDev) return ANNETY_CRC_ENODEV;
@@ -1058,35 +913,22 @@ int annety_crc_shutdown(void) {
     }
     {
       std::lock_guard<std::mutex> al(c.arena_mu);
-      // shutdown is the one place that drains the device: the slots' last uses carry no event
-      if (!c.slots.empty()) {
+      // the slots' last uses may carry no event: drain the device before their memory goes
+      if (c.slots.size()) {
         (void)hipDeviceSynchronize();
-        c.device_syncs++;
+        c.shutdown_syncs++;
       }
-      for (auto& sl : c.slots) {
-        if (sl->ptr) (void)hipFree(sl->ptr);
-        if (sl->hint) (void)hipHostFree(sl->hint);
-        (void)hipEventDestroy(sl->fence);
-      }
-      c.slots.clear();
+      HipSlotOps ops;
+      c.slots.clear(ops, [](ScratchSlot& sl) {
+        if (sl.data.ptr) (void)hipFree(sl.data.ptr);
+        if (sl.data.hint) (void)hipHostFree(sl.data.hint);
+      });
     }
     free_images(c);
     c.ready = false;
   }
   (void)hipSetDevice(prev);
   return ANNETY_CRC_OK;
-}
-
-const char* annety_crc_strerror(int status) {
-  switch (status) {
-    case ANNETY_CRC_OK: return "ok";
-    case ANNETY_CRC_EINVAL: return "invalid argument";
-    case ANNETY_CRC_EHIP: return "HIP runtime error";
-    case ANNETY_CRC_ENOMEM: return "out of memory";
-    case ANNETY_CRC_ENODEV: return "no usable gfx950 device";
-    case ANNETY_CRC_ERCCL: return "collective failure";
-    default: return "unknown status";
-  }
 }
 
 int annety_crc_last_hip_error(void) { return t_last_hip; }
@@ -1108,12 +950,10 @@ int annety_crc_set_split(int mode, uint64_t min_segment) {
 int annety_crc_scratch_stats(int device, uint64_t* slots, uint64_t* handoffs, uint64_t* device_syncs) {
   if (device < 0 || device >= kMaxDev) return ANNETY_CRC_ENODEV;
   DeviceCtx& c = g_dev[device];
-  {
-    std::lock_guard<std::mutex> lk(c.arena_mu);
-    if (slots) *slots = c.slots.size();
-  }
-  if (handoffs) *handoffs = c.handoffs.load();
-  if (device_syncs) *device_syncs = c.device_syncs.load();
+  std::lock_guard<std::mutex> lk(c.arena_mu);
+  if (slots) *slots = c.slots.size();
+  if (handoffs) *handoffs = c.slots.handoffs();
+  if (device_syncs) *device_syncs = c.slots.drains() + c.shutdown_syncs.load();
   return ANNETY_CRC_OK;
 }
 
@@ -1131,55 +971,17 @@ int annety_crc_stream_release(void* stream) {
   int rc = stream_ctx(s, &c);
   if (rc) return rc;
   std::lock_guard<std::mutex> lk(c->arena_mu);
-  for (size_t i = 0; i < c->slots.size(); i++) {
-    DeviceCtx::ScratchSlot& sl = *c->slots[i];
-    if (!same_owner(sl, s)) continue;
+  HipSlotOps ops;
+  return c->slots.release(ops, s, s == hipStreamPerThread, [&](ScratchSlot& sl) -> int {
     // stream-ordered: the memory returns to the pool after the stream's queued work, nobody waits
-    if (sl.ptr) HIP_TRY(hipFreeAsync(sl.ptr, s));
-    if (sl.hint) {  // the stream's queued extent kernels may still write it: wait for them first
+    if (sl.data.ptr) HIP_TRY(hipFreeAsync(sl.data.ptr, s));
+    if (sl.data.hint) {  // the stream's queued extent kernels may still write it: wait for them first
       HIP_TRY(hipStreamSynchronize(s));
-      (void)hipHostFree(sl.hint);
+      (void)hipHostFree(sl.data.hint);
     }
-    (void)hipEventDestroy(sl.fence);
-    c->slots.erase(c->slots.begin() + (long)i);
-    break;
-  }
-  return ANNETY_CRC_OK;
+    return ANNETY_CRC_OK;
+  });
 }
-
-// include/Crc32c.h:58-69
-uint32_t annety_crc32_long(const char* buff, size_t len) {
-  const unsigned char* p = reinterpret_cast<const unsigned char*>(buff);
-  uint32_t crc = kInit;
-  while (len--) crc = annety::internal::crc32_table256[(crc ^ *p++) & 0xff] ^ (crc >> 8);
-  return crc ^ kXorOut;
-}
-
-// include/Crc32c.h:41-55
-uint32_t annety_crc32_short(const char* buff, size_t len) {
-  const unsigned char* p = reinterpret_cast<const unsigned char*>(buff);
-  uint32_t crc = kInit;
-  while (len--) {
-    const unsigned c = *p++;
-    crc = annety::internal::crc32_table16[(crc ^ (c & 0xf)) & 0xf] ^ (crc >> 4);
-    crc = annety::internal::crc32_table16[(crc ^ (c >> 4)) & 0xf] ^ (crc >> 4);
-  }
-  return crc ^ kXorOut;
-}
-
-// include/Crc32c.h:71-82
-void annety_crc32_update(uint32_t* crc, const char* buff, size_t len) {
-  if (!crc) return;
-  const unsigned char* p = reinterpret_cast<const unsigned char*>(buff);
-  uint32_t c = *crc;
-  while (len--) c = annety::internal::crc32_table256[(c ^ *p++) & 0xff] ^ (c >> 8);
-  *crc = c;
-}
-
-uint32_t annety_crc32_combine(uint32_t crc_a, uint32_t crc_b, uint64_t len_b) { return combine(crc_a, crc_b, len_b); }
-
-const uint32_t* annety_crc32_table16(void) { return annety::internal::crc32_table16; }
-const uint32_t* annety_crc32_table256(void) { return annety::internal::crc32_table256; }
 
 int annety_crc32_batch_fixed(const void* d_base, size_t n, size_t len, size_t stride, uint32_t* d_out,
                              void* stream) {
@@ -1342,255 +1144,28 @@ int annety_crc32_batch_fixed_host(const void* h_base, size_t n, size_t len, size
   return ANNETY_CRC_OK;
 }
 
+// Pins [h_ptr, h_ptr + bytes) for in-place DMA. The library records the range (crc32_host.h HostRegistry) and
+// refuses a pointer that is not page-aligned or a range that shares a page with one it already pinned: the
+// runtime pins whole pages, and two registrations sharing a page leave it a lookup it can resolve to either.
 int annety_crc_host_register(void* h_ptr, size_t bytes) {
-  if (!h_ptr || !bytes) return ANNETY_CRC_EINVAL;
-  HIP_TRY(hipHostRegister(h_ptr, bytes, hipHostRegisterDefault));
+  if (!host::host_registry().add(h_ptr, bytes)) return ANNETY_CRC_EINVAL;
+  const hipError_t e = hipHostRegister(h_ptr, bytes, hipHostRegisterDefault);
+  if (e != hipSuccess) {
+    host::host_registry().drop(h_ptr);
+    return hip_fail(e);
+  }
   return ANNETY_CRC_OK;
 }
 
 int annety_crc_host_unregister(void* h_ptr) {
-  if (!h_ptr) return ANNETY_CRC_EINVAL;
+  if (!h_ptr || !host::host_registry().drop(h_ptr)) return ANNETY_CRC_EINVAL;  // not a range pinned here
   HIP_TRY(hipHostUnregister(h_ptr));
   return ANNETY_CRC_OK;
 }
 
-// ---- LengthHeaderCodec frames ----
-static bool lhc_type_ok(int t) { return t == 1 || t == 2 || t == 4 || t == 8; }
+const char* annety_crc_last_error_stage(void) { return t_fail_stage; }
 
-// include/codec/LengthHeaderCodec.h:71-137 without the CRC: signed big-endian length (peek_int*),
-// min_payload = checksum_length = 4, max_payload check, completeness check.
-// Framing rules of annety's two CRC codecs (same wire layout [len T BE][payload][crc BE]):
-//   decode: length (payload + 4) outside [dec_min, dec_max] is invalid (decode -1); dec_max <= 0: no limit
-//   encode: payload length 0 -> rt 0; outside [enc_min, enc_max] -> rt -1; enc_max <= 0: no limit
-struct FrameRules {
-  int T;
-  int64_t dec_min, dec_max, enc_min, enc_max;
-};
-// LengthHeaderCodec (include/codec/LengthHeaderCodec.h): min_payload() = checksum_length() = 4 (:214-217),
-// max_payload checked only when > 0 (:102, :174), decode :71-137, encode :146-201.
-static FrameRules lhc_rules(int T, int64_t max_payload) { return {T, 4, max_payload, 1, max_payload}; }
-// ProtobufCodec (include/protobuf/ProtobufCodec.h): T = kLengthType32 (:260-263), min_payload() =
-// header_length() 4 + 2 + checksum_length() 4 = 10 (:279-283), max_payload() = 64 MiB unconditional
-// (:273-277); decode rejects length < 10 or > 64 MiB (:149-153), encode rejects payload < 10 - 4 = 6 or
-// > 64 MiB (:229-233).
-static constexpr FrameRules kPbcRules = {4, 10, 64ll << 20, 6, 64ll << 20};
-
-// ---- frame walks: LengthHeaderCodec::decode's framing (include/codec/LengthHeaderCodec.h:71-137) over a
-// host buffer, a dependent chain of one header read per frame (~140-170 ns a frame from DRAM) ----
-// A buffer of at least two walk segments (annety_crc_set_walk_segment, default 64 MiB) is walked in
-// segments side by side. Segment 0 is walked from offset 0 as the codec does. Every later segment first
-// looks for a speculative entry: the first position in its first kSpecProbe bytes from which kSpecHops
-// frames in a row parse. It walks from there to its end. The walks are then joined in order: the true walk
-// (from offset 0) continues frame by frame until it lands on a header the next segment's walk recorded;
-// from that header on, both walks are the same chain, so that segment's frames are taken as they are. A
-// segment whose entry was wrong (payload bytes that parse as headers) is walked again by the join, frame by
-// frame: speculation costs time, never a different result.
-namespace {
-enum class Step { kFrame, kInvalid, kIncomplete, kTooBig };
-
-// The frame whose header starts at `pos`; *length = its length field (payload + 4 checksum bytes).
-inline Step frame_at(const FrameRules& r, const unsigned char* p, size_t size, size_t pos, int64_t* length) {
-  const size_t T = (size_t)r.T;
-  if (pos > size || size - pos < T) return Step::kIncomplete;
-  uint64_t u = 0;
-  for (size_t b = 0; b < T; b++) u = (u << 8) | p[pos + b];
-  switch (T) {  // sign-extend like peek_int8/16/32/64
-    case 1: *length = (int8_t)u; break;
-    case 2: *length = (int16_t)u; break;
-    case 4: *length = (int32_t)u; break;
-    default: *length = (int64_t)u; break;
-  }
-  if (*length < r.dec_min || (r.dec_max > 0 && *length > r.dec_max)) return Step::kInvalid;  // decode: -1
-  if (size - pos - T < (uint64_t)*length) return Step::kIncomplete;                           // decode: 0
-  if (*length - 4 > 0xFFFFFFFFll) return Step::kTooBig;  // valid for the codec, beyond 32-bit lengths
-  return Step::kFrame;
-}
-inline int step_rt(Step s) { return s == Step::kInvalid ? 1 : s == Step::kTooBig ? ANNETY_CRC_EINVAL : 0; }
-
-struct ConnWalk {
-  std::vector<uint64_t> off;  // payload offsets, relative to the buffer
-  std::vector<uint32_t> len;
-  size_t consumed = 0;        // where the walk stopped
-  int rt = 0;                 // 0, 1 (invalid length) or ANNETY_CRC_EINVAL (a frame beyond 32-bit lengths)
-  bool ended = false;         // stopped by the stream itself, not by its stop position or the frame cap
-};
-
-// Frames from header position `pos` while pos < stop_at, at most `cap` of them in w.
-void walk_range(const FrameRules& r, const unsigned char* p, size_t size, size_t pos, size_t stop_at, size_t cap,
-                ConnWalk& w) {
-  const size_t T = (size_t)r.T;
-  while (pos < stop_at && w.off.size() < cap) {
-    int64_t L = 0;
-    const Step st = frame_at(r, p, size, pos, &L);
-    if (st != Step::kFrame) {
-      w.ended = true;
-      w.rt = step_rt(st);
-      break;
-    }
-    w.off.push_back(pos + T);
-    w.len.push_back((uint32_t)(L - 4));
-    pos += T + (size_t)L;
-  }
-  w.consumed = pos;
-}
-
-std::atomic<uint64_t> g_walk_seg{64ull << 20};
-constexpr size_t kWalkMaxSegs = 64;
-constexpr size_t kSpecProbe = 1u << 20;
-
-// Segment [lo, hi) of a buffer (not the first): a speculative entry, then the walk from it up to hi.
-void walk_segment(const FrameRules& r, const unsigned char* p, size_t size, size_t lo, size_t hi, size_t cap,
-                  ConnWalk& w) {
-  const size_t T = (size_t)r.T;
-  const int hops = T == 1 ? 32 : T == 2 ? 16 : 8;  // short length fields parse by chance more often
-  const size_t end = std::min(size, lo + kSpecProbe);
-  for (size_t q = lo; q < end; q++) {
-    size_t pos = q;
-    int h = 0;
-    int64_t L = 0;
-    for (; h < hops && frame_at(r, p, size, pos, &L) == Step::kFrame; h++) pos += T + (size_t)L;
-    if (h == hops) {
-      walk_range(r, p, size, q, hi, cap, w);
-      return;
-    }
-  }
-  w.consumed = SIZE_MAX;  // no entry found: the join walks this segment itself
-}
-
-// The walks of k buffers, on walker threads; join() leaves walks()[c] = buffer c's walk from offset 0.
-class FrameWalks {
- public:
-  FrameWalks(const FrameRules& r, const void* const* bufs, const size_t* sizes, size_t k, size_t cap)
-      : r_(r), bufs_(bufs), sizes_(sizes), cap_(cap), bounds_(k), segs_(k), walks_(k) {
-    const size_t seg = (size_t)g_walk_seg.load();
-    for (size_t c = 0; c < k; c++) {
-      const size_t m = std::max<size_t>(1, std::min<size_t>(kWalkMaxSegs, sizes[c] / seg));
-      bounds_[c].resize(m + 1);
-      for (size_t i = 0; i < m; i++) bounds_[c][i] = sizes[c] / m * i;
-      bounds_[c][m] = SIZE_MAX;  // the last segment walks to the stream's end
-      segs_[c].resize(m);
-      for (size_t i = 0; i < m; i++) tasks_.push_back({c, i});
-    }
-  }
-  ~FrameWalks() { join_threads(); }
-  // The walks start on walk_pool()'s workers.
-  void start() { job_ = walk_pool().submit(tasks_.size(), [this](size_t i) { run(tasks_[i]); }); }
-  void join() {  // idempotent; the caller takes any walks still queued
-    join_threads();
-    if (joined_) return;
-    joined_ = true;
-    for (size_t c = 0; c < walks_.size(); c++) splice(c);
-  }
-  std::vector<ConnWalk>& walks() { return walks_; }
-
- private:
-  struct Task {
-    size_t c, i;
-  };
-  const unsigned char* buf(size_t c) const { return static_cast<const unsigned char*>(bufs_[c]); }
-  void run(const Task& t) {
-    const size_t lo = bounds_[t.c][t.i], hi = bounds_[t.c][t.i + 1];
-    if (t.i == 0)
-      walk_range(r_, buf(t.c), sizes_[t.c], 0, hi, cap_, segs_[t.c][0]);
-    else
-      walk_segment(r_, buf(t.c), sizes_[t.c], lo, hi, cap_, segs_[t.c][t.i]);
-  }
-  void join_threads() {
-    if (job_) walk_pool().wait(*job_);
-    job_.reset();
-  }
-  void splice(size_t c) {
-    std::vector<ConnWalk>& segs = segs_[c];
-    ConnWalk& out = walks_[c];
-    out = std::move(segs[0]);
-    const unsigned char* p = buf(c);
-    const size_t size = sizes_[c], T = (size_t)r_.T;
-    size_t pos = out.consumed;
-    for (size_t i = 1; i < segs.size() && !out.ended && out.off.size() < cap_; i++) {
-      ConnWalk& s = segs[i];
-      const size_t hi = bounds_[c][i + 1];
-
-      while (!out.ended && out.off.size() < cap_ && pos < hi) {
-        const auto it = std::lower_bound(s.off.begin(), s.off.end(), (uint64_t)pos + T);
-        if (it != s.off.end() && *it == pos + T) {  // the true walk reached a header of the segment's walk
-          const size_t j = (size_t)(it - s.off.begin());
-          const size_t take = std::min(s.off.size() - j, cap_ - out.off.size());
-          out.off.insert(out.off.end(), s.off.begin() + j, s.off.begin() + j + take);
-          out.len.insert(out.len.end(), s.len.begin() + j, s.len.begin() + j + take);
-          if (j + take < s.off.size()) {  // cut by the frame cap
-            pos = out.off.back() + out.len.back() + 4;
-            break;
-          }
-          pos = s.consumed;  // the segment's end, its own cap (go on frame by frame) or the stream's end
-          if (s.ended) {
-            out.ended = true;
-            out.rt = s.rt;
-          }
-          continue;
-        }
-        int64_t L = 0;
-        const Step st = frame_at(r_, p, size, pos, &L);
-        if (st != Step::kFrame) {
-          out.ended = true;
-          out.rt = step_rt(st);
-          break;
-        }
-        out.off.push_back(pos + T);
-        out.len.push_back((uint32_t)(L - 4));
-        pos += T + (size_t)L;
-      }
-    }
-    out.consumed = pos;
-    segs.clear();
-  }
-
-  const FrameRules r_;
-  const void* const* bufs_;
-  const size_t* sizes_;
-  const size_t cap_;
-  std::vector<std::vector<size_t>> bounds_;
-  std::vector<std::vector<ConnWalk>> segs_;
-  std::vector<ConnWalk> walks_;
-  std::vector<Task> tasks_;
-  std::unique_ptr<WorkPool::Job> job_;
-  bool joined_ = false;
-};
-
-}  // namespace
-
-static int parse_frames(const FrameRules& r, const void* h_stream, size_t size, uint64_t* payload_off,
-                        uint32_t* payload_len, size_t max_frames, size_t* n_frames, size_t* consumed) {
-  if (!n_frames || !consumed || !lhc_type_ok(r.T) || (!h_stream && size) || (max_frames && (!payload_off || !payload_len)))
-    return ANNETY_CRC_EINVAL;
-  FrameWalks fw(r, &h_stream, &size, 1, max_frames);
-  fw.start();
-  fw.join();
-  const ConnWalk& w = fw.walks()[0];
-  std::copy(w.off.begin(), w.off.end(), payload_off);
-  std::copy(w.len.begin(), w.len.end(), payload_len);
-  *n_frames = w.off.size();
-  *consumed = w.consumed;
-  return w.rt;
-}
-
-int annety_crc_set_walk_segment(uint64_t bytes) {
-  if (bytes && bytes < 4096) return ANNETY_CRC_EINVAL;
-  g_walk_seg.store(bytes ? bytes : 64ull << 20);
-  return ANNETY_CRC_OK;
-}
-
-// include/codec/LengthHeaderCodec.h:71-137 without the CRC: signed big-endian length (peek_int*),
-// min_payload = checksum_length = 4, max_payload check, completeness check.
-int annety_lhc_parse(const void* h_stream, size_t size, int length_type, int64_t max_payload, uint64_t* payload_off,
-                     uint32_t* payload_len, size_t max_frames, size_t* n_frames, size_t* consumed) {
-  return parse_frames(lhc_rules(length_type, max_payload), h_stream, size, payload_off, payload_len, max_frames,
-                      n_frames, consumed);
-}
-
-int annety_pbc_parse(const void* h_stream, size_t size, uint64_t* payload_off, uint32_t* payload_len,
-                     size_t max_frames, size_t* n_frames, size_t* consumed) {
-  return parse_frames(kPbcRules, h_stream, size, payload_off, payload_len, max_frames, n_frames, consumed);
-}
+const char* annety_crc_last_kernels(void) { return t_kernels.c_str(); }
 
 static int lhc_verify(const void* d_stream, size_t stream_bytes, bool arena, const uint64_t* d_payload_off,
                       const uint32_t* d_payload_len, size_t n, uint8_t* d_ok, uint32_t* d_digest, void* stream) {
@@ -1626,25 +1201,6 @@ int annety_lhc_verify_stream(const void* d_stream, size_t stream_bytes, const ui
   return lhc_verify(d_stream, stream_bytes, true, d_payload_off, d_payload_len, n, d_ok, d_digest, stream);
 }
 
-// encode()'s per-payload decision (LengthHeaderCodec :169-176, ProtobufCodec :225-233): rt 0 for an empty
-// payload, -1 outside [enc_min, enc_max], else 1 with a frame of T + len + 4 bytes. Rejected payloads
-// get zero bytes, so the frames of the accepted ones are packed back to back as consecutive encode
-// calls on one NetBuffer would leave them.
-static int encode_plan(const FrameRules& r, const uint32_t* h_len, size_t n, uint64_t* h_frame_off, int8_t* h_rt,
-                       uint64_t* total) {
-  if (!lhc_type_ok(r.T) || !total || (n && (!h_len || !h_frame_off))) return ANNETY_CRC_EINVAL;
-  uint64_t pos = 0;
-  for (size_t i = 0; i < n; i++) {
-    const int64_t L = h_len[i];
-    const int8_t rt = L == 0 ? 0 : (L < r.enc_min || (r.enc_max > 0 && L > r.enc_max)) ? -1 : 1;
-    if (h_rt) h_rt[i] = rt;
-    h_frame_off[i] = pos;
-    if (rt == 1) pos += (uint64_t)r.T + (uint64_t)L + 4;
-  }
-  *total = pos;
-  return ANNETY_CRC_OK;
-}
-
 static int encode_batch(const FrameRules& r, const void* d_src, const uint64_t* d_src_off, const uint32_t* d_len,
                         size_t n, void* d_dst, const uint64_t* d_frame_off, void* stream) {
   if (n == 0) return ANNETY_CRC_OK;
@@ -1665,19 +1221,10 @@ static int encode_batch(const FrameRules& r, const void* d_src, const uint64_t* 
   return rc;
 }
 
-int annety_lhc_encode_plan(const uint32_t* h_len, size_t n, int length_type, int64_t max_payload,
-                           uint64_t* h_frame_off, int8_t* h_rt, uint64_t* total) {
-  return encode_plan(lhc_rules(length_type, max_payload), h_len, n, h_frame_off, h_rt, total);
-}
-
 int annety_lhc_encode_batch(const void* d_src, const uint64_t* d_src_off, const uint32_t* d_len, size_t n,
                             int length_type, int64_t max_payload, void* d_dst, const uint64_t* d_frame_off,
                             void* stream) {
   return encode_batch(lhc_rules(length_type, max_payload), d_src, d_src_off, d_len, n, d_dst, d_frame_off, stream);
-}
-
-int annety_pbc_encode_plan(const uint32_t* h_len, size_t n, uint64_t* h_frame_off, int8_t* h_rt, uint64_t* total) {
-  return encode_plan(kPbcRules, h_len, n, h_frame_off, h_rt, total);
 }
 
 int annety_pbc_encode_batch(const void* d_src, const uint64_t* d_src_off, const uint32_t* d_len, size_t n,
@@ -1692,16 +1239,19 @@ int annety_pbc_encode_batch(const void* d_src, const uint64_t* d_src_off, const 
 // its own walker thread (connections are independent), while the buffers are packed into pinned memory
 // and uploaded (pinned buffers, e.g. annety_crc_host_register'ed NetBuffer arenas, are DMA'd in place).
 // Pageable frame buffers: packed into the library's pinned ring by the pack threads (default), or uploaded by
-// the runtime's own pageable copy (ANNETY_CRC_FRAMES_PACK=0). The runtime pins a large pageable source for
-// the length of its copy; K receive buffers allocated next to each other can share a page, and two such copies
-// in flight then pin and unpin the same page - the suspected cause of the intermittent illegal address in
-// the K-connection test. The pack never hands a user page to the DMA engine. Read once.
-static bool frames_pageable_direct() {
-  static const bool direct = [] {
-    const char* e = std::getenv("ANNETY_CRC_FRAMES_PACK");
-    return e && e[0] == '0';
-  }();
-  return direct;
+// the runtime's own pageable copy (annety_crc_set_frames_pack(0); initial value from ANNETY_CRC_FRAMES_PACK).
+// The pack never hands a user page to the DMA engine, so the runtime's pinning of user memory (which keys on
+// pages that neighbouring buffers and earlier registrations may share) stays out of this path.
+static std::atomic<int> g_frames_pack{[] {
+  const char* e = std::getenv("ANNETY_CRC_FRAMES_PACK");
+  return (e && e[0] == '0') ? 0 : 1;
+}()};
+
+// ANNETY_CRC_SYNC_STAGES=1: finish the stage's queued work now, so a failure is charged to it.
+static int stage_sync(hipStream_t s) {
+  if (!sync_stages()) return ANNETY_CRC_OK;
+  const hipError_t e = hipStreamSynchronize(s);
+  return e == hipSuccess ? ANNETY_CRC_OK : hip_fail(e);
 }
 
 static int verify_host_iov(const FrameRules& r, const void* const* h_bufs, const size_t* sizes, size_t k,
@@ -1732,6 +1282,7 @@ static int verify_host_iov(const FrameRules& r, const void* const* h_bufs, const
   }
   std::unique_lock<std::mutex> lk(c->stg_mu);
   Staging& st = c->stg;
+  set_stage("staging buffers");
   auto fail = [&](int status) {
     join_walkers();
     if (st.stream[0]) (void)hipStreamSynchronize(st.stream[0]);
@@ -1750,7 +1301,8 @@ static int verify_host_iov(const FrameRules& r, const void* const* h_bufs, const
   hipStream_t s = st.stream[0];
   bool pinned = true;
   for (size_t i = 0; i < k && pinned; i++) pinned = !sizes[i] || host_pinned(h_bufs[i], sizes[i]);
-  if (pinned || frames_pageable_direct()) {
+  set_stage(pinned ? "upload (pinned, in place)" : g_frames_pack.load() ? "upload (packed)" : "upload (pageable)");
+  if (pinned || !g_frames_pack.load()) {
     for (size_t i = 0; i < k; i++) {
       if (!sizes[i]) continue;
       const hipError_t e = hipMemcpyAsync(st.d_stream + base[i], h_bufs[i], sizes[i], hipMemcpyHostToDevice, s);
@@ -1779,6 +1331,8 @@ static int verify_host_iov(const FrameRules& r, const void* const* h_bufs, const
       if (e != hipSuccess) return fail(hip_fail(e));
     }
   }
+  if ((rc = stage_sync(s))) return fail(rc);
+  set_stage("walk join");
   join_walkers();
   std::vector<ConnWalk>& walks = fw.walks();
   // frames in connection order, the output bound applied in that order (Codec::recv's per-connection
@@ -1808,6 +1362,7 @@ static int verify_host_iov(const FrameRules& r, const void* const* h_bufs, const
     return prc;
   }
   if (nf) {
+    set_stage("metadata buffers");
     if (st.meta_cap < nf) {
       if (st.d_meta) (void)hipFree(st.d_meta);
       st.d_meta = nullptr;
@@ -1833,19 +1388,36 @@ static int verify_host_iov(const FrameRules& r, const void* const* h_bufs, const
     uint32_t* d_len = reinterpret_cast<uint32_t*>(st.d_meta + nf * 8);
     uint32_t* d_dig = d_len + nf;
     uint8_t* d_ok = reinterpret_cast<uint8_t*>(d_dig + nf);
+    set_stage("metadata upload");
     hipError_t e = hipMemcpyAsync(d_off, st.h_meta, nf * 12, hipMemcpyHostToDevice, s);  // off then len
     if (e != hipSuccess) return fail(hip_fail(e));
+    if ((rc = stage_sync(s))) return fail(rc);
+    set_stage("arena verify");
     rc = run_arena(*c, st.d_stream, total, d_off, d_len, nf, d_dig, s, false);
+    if (rc == ANNETY_CRC_OK) rc = stage_sync(s);
     if (rc == ANNETY_CRC_OK) {
+      set_stage("trailer compare");
       e = launch_lhc_compare(st.d_stream, d_off, d_len, nf, d_dig, d_ok, s);
-      if (e == hipSuccess) e = hipMemcpyAsync(st.h_meta + nf * 12, d_ok, nf, hipMemcpyDeviceToHost, s);
+      if (e != hipSuccess) rc = hip_fail(e);
+      if (rc == ANNETY_CRC_OK) rc = stage_sync(s);
+    }
+    if (rc == ANNETY_CRC_OK) {
+      set_stage("verdict download");
+      e = hipMemcpyAsync(st.h_meta + nf * 12, d_ok, nf, hipMemcpyDeviceToHost, s);
       if (e != hipSuccess) rc = hip_fail(e);
     }
   }
+  set_stage("final sync");
   const hipError_t e = hipStreamSynchronize(s);
   if (rc == ANNETY_CRC_OK && e != hipSuccess) rc = hip_fail(e);
   if (rc == ANNETY_CRC_OK && nf) std::memcpy(h_ok, st.h_meta + nf * 12, nf);
   return rc;
+}
+
+int annety_crc_set_frames_pack(int pack) {
+  if (pack != 0 && pack != 1) return ANNETY_CRC_EINVAL;
+  g_frames_pack.store(pack);
+  return ANNETY_CRC_OK;
 }
 
 // One receive buffer: the K = 1 case of verify_host_iov.

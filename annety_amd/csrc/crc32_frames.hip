@@ -73,6 +73,7 @@ hipError_t launch_lhc_compare(const void* stream_base, const uint64_t* off, cons
                               const uint32_t* digest, uint8_t* ok, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   const unsigned blocks = (unsigned)((n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096);
+  note_kernel("lhc_compare_kernel");
   hipLaunchKernelGGL(lhc_compare_kernel, dim3(blocks), dim3(256), 0, stream,
                      static_cast<const uint8_t*>(stream_base), off, len, n, digest, ok);
   return hipGetLastError();
@@ -83,6 +84,7 @@ hipError_t launch_lhc_encode(const void* src, const uint64_t* src_off, const uin
                              const uint32_t* digest, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   const unsigned blocks = (unsigned)((n + 3) / 4 < 8192 ? (n + 3) / 4 : 8192);
+  note_kernel("lhc_encode_kernel");
   hipLaunchKernelGGL(lhc_encode_kernel, dim3(blocks), dim3(256), 0, stream, static_cast<const uint8_t*>(src),
                      src_off, len, n, T, enc_min, enc_max, static_cast<uint8_t*>(dst), dst_off, digest);
   return hipGetLastError();

@@ -2,7 +2,7 @@
 // group of gfx950 devices, the way one annety process runs N event loops (src/EventLoopPool.cc:55-66)
 // but with the batch sharded over GPUs instead of threads.
 //
-//  * annety_crc_shard_plan: contiguous block shards, balanced to within one payload.
+//  * annety_crc_shard_plan (host only, crc32_host.cpp): contiguous block shards, balanced to within one payload.
 //  * annety_crc32_group_batch_fixed: device-resident shards; each device checksums its shard chunk by
 //    chunk on its own stream, and chunk c's digests travel to the root device over RCCL (xGMI) on a
 //    communication stream while chunk c+1 is computed. The communicator is ncclCommInitAll over the
@@ -55,16 +55,15 @@ struct DeviceGuard {  // restores the caller's current device
   ~DeviceGuard() { (void)hipSetDevice(prev); }
 };
 
-void chunk_of(size_t n, size_t chunks, size_t c, size_t* lo, size_t* hi) {
-  *lo = n * c / chunks;
-  *hi = n * (c + 1) / chunks;
-}
-
 void release(annety_crc_group* g) {
   for (size_t k = 0; k < g->dev.size(); k++) {
     (void)hipSetDevice(g->dev[k]);
     if (k < g->comm.size() && g->comm[k]) (void)ncclCommDestroy(g->comm[k]);
-    if (k < g->compute.size() && g->compute[k]) (void)hipStreamDestroy(g->compute[k]);
+    if (k < g->compute.size() && g->compute[k]) {
+      // the split path may hold a scratch slot keyed on this stream: drop it while the stream is alive
+      (void)annety_crc_stream_release(g->compute[k]);
+      (void)hipStreamDestroy(g->compute[k]);
+    }
     if (k < g->comms.size() && g->comms[k]) (void)hipStreamDestroy(g->comms[k]);
     if (k < g->ready.size() && g->ready[k]) (void)hipEventDestroy(g->ready[k]);
     if (k < g->scratch.size() && g->scratch[k]) (void)hipFree(g->scratch[k]);
@@ -75,16 +74,7 @@ void release(annety_crc_group* g) {
 
 extern "C" {
 
-int annety_crc_shard_plan(size_t n, int nshards, size_t* first, size_t* count) {
-  if (nshards <= 0 || !first || !count) return ANNETY_CRC_EINVAL;
-  for (int k = 0; k < nshards; k++) {
-    const size_t lo = (size_t)((unsigned __int128)n * (unsigned)k / (unsigned)nshards);
-    const size_t hi = (size_t)((unsigned __int128)n * (unsigned)(k + 1) / (unsigned)nshards);
-    first[k] = lo;
-    count[k] = hi - lo;
-  }
-  return ANNETY_CRC_OK;
-}
+// annety_crc_shard_plan and annety_crc_group_schedule are host-only: crc32_host.cpp.
 
 int annety_crc_group_create(const int* devices, int ndev, annety_crc_group** out) {
   if (!devices || ndev <= 0 || !out) return ANNETY_CRC_EINVAL;
@@ -139,23 +129,6 @@ int annety_crc_group_destroy(annety_crc_group* g) {
 }
 
 int annety_crc_group_size(const annety_crc_group* g) { return g ? (int)g->dev.size() : 0; }
-
-int annety_crc_group_schedule(const size_t* n_shard, int nd, size_t chunks, size_t* plan) {
-  if (!n_shard || nd <= 0 || chunks == 0 || !plan) return ANNETY_CRC_EINVAL;
-  size_t base = 0;
-  for (int k = 0; k < nd; k++) {
-    for (size_t c = 0; c < chunks; c++) {
-      size_t lo, hi;
-      chunk_of(n_shard[k], chunks, c, &lo, &hi);
-      size_t* e = plan + (c * (size_t)nd + (size_t)k) * 3;
-      e[0] = lo;         // first payload of the piece, within shard k
-      e[1] = hi - lo;    // payloads in the piece (0: nothing to compute or move)
-      e[2] = base + lo;  // where its digests land in the root's output
-    }
-    base += n_shard[k];
-  }
-  return ANNETY_CRC_OK;
-}
 
 int annety_crc32_group_batch_fixed(annety_crc_group* g, const void* const* d_shard, const size_t* n_shard, size_t len,
                                    size_t stride, uint32_t* d_root_out, size_t chunks) {

@@ -198,5 +198,7 @@ hipError_t launch_lhc_encode(const void* src, const uint64_t* src_off, const uin
                              int64_t enc_min, int64_t enc_max, void* dst, const uint64_t* dst_off,
                              const uint32_t* digest, hipStream_t stream);
 int fixed_kernel_block();
+// Records, for annety_crc_last_kernels, that the current entry point enqueued `name` (crc32_capi.cpp).
+void note_kernel(const char* name);
 
 }  // namespace annety_crc

@@ -709,6 +709,8 @@ hipError_t launch_var_g(const VarLaunch& a, hipStream_t stream) {
     blocks = std::min(blocks, (lanes + kBlock - 1) / kBlock);
   }
   if (blocks == 0) return hipSuccess;
+  note_kernel(G == 1 ? "crc32_var_kernel<1>" : G == 2 ? "crc32_var_kernel<2>" : G == 4 ? "crc32_var_kernel<4>" :
+              G == 8 ? "crc32_var_kernel<8>" : G == 16 ? "crc32_var_kernel<16>" : "crc32_var_kernel<32>");
 #define ANNETY_VAR_LAUNCH(SORTED, UPD)                                                                     \
   hipLaunchKernelGGL((crc32_var_kernel<G, SORTED, UPD>), dim3((unsigned)blocks), dim3(kBlock), 0, stream,   \
                      static_cast<const uint8_t*>(a.base), a.n, a.fixed_stride, a.fixed_len,                  \
@@ -732,6 +734,8 @@ hipError_t launch_g(const FixedLaunch& a, hipStream_t stream) {
   size_t blocks = (lanes + kBlock - 1) / kBlock;
   if (blocks > a.max_blocks) blocks = a.max_blocks;
   if (blocks == 0) return hipSuccess;
+  note_kernel(G == 1 ? "crc32_fixed_kernel<1>" : G == 2 ? "crc32_fixed_kernel<2>" : G == 4 ? "crc32_fixed_kernel<4>" :
+              G == 8 ? "crc32_fixed_kernel<8>" : G == 16 ? "crc32_fixed_kernel<16>" : "crc32_fixed_kernel<32>");
   hipLaunchKernelGGL((crc32_fixed_kernel<G, FULL, RAW>), dim3((unsigned)blocks), dim3(kBlock), 0, stream,
                      static_cast<const uint8_t*>(a.base), a.n, a.stride, a.rounds, a.vlead,
                      static_cast<const uint4*>(a.img_slice), static_cast<const uint4*>(a.img_group), a.raw_shift_cols,
@@ -745,6 +749,9 @@ hipError_t launch_one_g(const FixedLaunch& a, hipStream_t stream) {
   size_t blocks = (lanes + kBlock - 1) / kBlock;
   if (blocks > a.max_blocks) blocks = a.max_blocks;
   if (blocks == 0) return hipSuccess;
+  note_kernel(G == 1 ? "crc32_oneround_kernel<1>" : G == 2 ? "crc32_oneround_kernel<2>" :
+              G == 4 ? "crc32_oneround_kernel<4>" : G == 8 ? "crc32_oneround_kernel<8>" :
+              G == 16 ? "crc32_oneround_kernel<16>" : "crc32_oneround_kernel<32>");
   hipLaunchKernelGGL((crc32_oneround_kernel<G>), dim3((unsigned)blocks), dim3(kBlock), 0, stream,
                      static_cast<const uint8_t*>(a.base), a.n, a.stride, static_cast<const uint4*>(a.img_slice),
                      static_cast<const uint4*>(a.img_group), a.out);
@@ -766,6 +773,7 @@ hipError_t launch_one(const FixedLaunch& a, hipStream_t stream) {
     size_t blocks = (a.n * 8 + kBlock - 1) / kBlock;
     if (blocks > a.max_blocks) blocks = a.max_blocks;
     if (blocks == 0) return hipSuccess;
+    note_kernel("crc32_onekib_nt_kernel");
     hipLaunchKernelGGL((crc32_onekib_nt_kernel<>), dim3((unsigned)blocks), dim3(kBlock), 0, stream,
                        static_cast<const uint8_t*>(a.base), a.n, static_cast<const uint4*>(a.img_slice),
                        static_cast<const uint4*>(a.img_group), static_cast<const uint4*>(a.img_bytemap), a.out);
@@ -802,6 +810,7 @@ hipError_t launch_fixed(const FixedLaunch& a, hipStream_t stream) {
     size_t blocks = (a.n * 32 + kBlock - 1) / kBlock;
     if (blocks > a.max_blocks) blocks = a.max_blocks;
     if (blocks == 0) return hipSuccess;
+    note_kernel("crc32_fixed32_nt_kernel");
     hipLaunchKernelGGL((crc32_fixed32_nt_kernel<>), dim3((unsigned)blocks), dim3(kBlock), 0, stream,
                        static_cast<const uint8_t*>(a.base), a.n, a.stride, a.rounds,
                        static_cast<const uint4*>(a.img_slice), static_cast<const uint4*>(a.img_group),
@@ -816,6 +825,7 @@ hipError_t launch_fixed(const FixedLaunch& a, hipStream_t stream) {
 hipError_t launch_var_sorted(const VarLaunch& a, const void* img_g32, const void* img_g16, const void* img_g4,
                              hipStream_t stream) {
   const unsigned blocks = (unsigned)std::max<size_t>(1, a.max_blocks);
+  note_kernel("crc32_var_sorted_kernel");
 #define ANNETY_SORTED_LAUNCH(UPD)                                                                             \
   hipLaunchKernelGGL((crc32_var_sorted_kernel<UPD>), dim3(blocks), dim3(kBlock), 0, stream,                  \
                      static_cast<const uint8_t*>(a.base), a.n, static_cast<const uint4*>(a.desc), a.range,      \
@@ -844,6 +854,7 @@ hipError_t launch_split_desc(const void* base, size_t n, uint64_t len, uint64_t 
                              void* desc, uint32_t* range, hipStream_t stream) {
   const size_t total = n * (size_t)S;
   const unsigned blocks = (unsigned)std::max<size_t>(1, std::min<size_t>(2048, (total + 255) / 256));
+  note_kernel("crc32_split_desc");
   hipLaunchKernelGGL(crc32_split_desc, dim3(blocks), dim3(256), 0, stream, static_cast<const uint8_t*>(base), n, len,
                      stride, seg, S, static_cast<uint4*>(desc), range);
   return hipGetLastError();
@@ -857,6 +868,7 @@ hipError_t launch_split_join(const uint32_t* seg_crc, size_t n, uint32_t S, cons
     if (e != hipSuccess) return e;
   }
   const unsigned blocks = (unsigned)std::max<size_t>(1, std::min<size_t>(8192, (units + 3) / 4));
+  note_kernel("crc32_split_join");
   hipLaunchKernelGGL(crc32_split_join, dim3(blocks), dim3(256), 0, stream, seg_crc, n, S, powers, out);
   return hipGetLastError();
 }

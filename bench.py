@@ -40,9 +40,12 @@ sys.path.insert(0, ROOT)
 
 METRIC = "CRC-32C GiB/s device-resident (1M×1KiB) @1/2/4/8 MI355X; % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md (8.0 TB/s)
-# Per-launch HBM bytes measured by profiles/pmc.sh at this code (FETCH_SIZE x2 + WRITE_SIZE), per config.
-PMC_FILES = {1: "profiles/r03/config1_pmc.json", 3: "profiles/r03/config3_pmc.json",
-             2: "profiles/r03/config2_pmc.json", 4: "profiles/r03/config1_pmc.json"}
+# Per-launch HBM bytes from the rocprofv3 PMC passes of this bench's own command (profiles/pmc.sh, FETCH_SIZE x2
+# gfx950 correction + WRITE_SIZE), committed per config; reported as `traffic` with the file as its source
+# (a PMC pass cannot run inside the timed process).
+PMC_FILES = {1: "profiles/r04/config1_pmc.json", 3: "profiles/r04/config3_pmc.json",
+             2: "profiles/r04/config2_pmc.json", 4: "profiles/r04/config1_pmc.json"}
+CPU_SAMPLE_BYTES = 1 << 30  # cpu_baseline sample: up to 1 GiB of the workload, far above the host's caches
 # The reference build of oracle/_ref (oracle/Makefile): the reference's Release flags without -march=native.
 REF_FLAGS = "g++ -std=c++11 -O2 -DNDEBUG (CMakeLists.txt:24,48 Release flags; -march=native dropped so the .so runs on any host)"
 
@@ -191,10 +194,6 @@ class Workload:
             self.payload_bytes = n * L
             self.algo_bytes = n * L + 4 * n  # payload reads + digest writes per launch
             self.offsets = self.lengths = None
-            if args.config == 2:
-                self.kernel = "crc32_fixed_kernel<32> over 64 KiB segments + crc32_split_join (annety_amd/csrc/crc32_kernels.hip)"
-            else:
-                self.kernel = "crc32_oneround_kernel<8> (annety_amd/csrc/crc32_kernels.hip)"
             # the workload only: identical at every N for a weak-scaling run, so the driver's N = 1..8 lines
             # are one curve (the gather, when there is one, is described in the line's "gather" object)
             if args.strong:
@@ -219,12 +218,6 @@ class Workload:
             self.algo_bytes = total + 4 * self.n + 12 * self.n  # + offset/length metadata reads
             self.arena = args.var_path == "arena"
             self.var_path = args.var_path
-            self.kernel = ("crc32_arena_lines_kernel + crc32_arena_stitch_kernel, one step "
-                           "(annety_amd/csrc/crc32_arena.hip, crc32_arena_lines.h)" if self.arena else
-                           "crc32_extent_kernel + (arena or sorted path, chosen per call), one step "
-                           "(annety_amd/csrc/crc32_capi.cpp run_var_auto)" if args.var_path == "auto" else
-                           "crc32_extent_kernel<count> + crc32_bucket_place + crc32_var_kernel<32/16/4>, one step "
-                           "(annety_amd/csrc/crc32_arena.hip, crc32_kernels.hip)")
             self.desc = (f"BASELINE config 3: {self.n} payloads, Zipf(1.1) lengths 64 B-64 KiB packed unaligned, "
                          f"{total / 2**30:.3f} GiB per GPU, " + {"arena": "arena path", "auto": "automatic path choice",
                                                                   "sorted": "sorted path"}[args.var_path])
@@ -232,6 +225,7 @@ class Workload:
         # largest so that every rank's gather moves the same count
         self.n_pad = -(-self.n_total // world) if getattr(args, "strong", False) else self.n
         self.out = torch.zeros(self.n_pad, dtype=torch.int32, device=dev)
+        self.kernel = None  # the kernels one step enqueues, as the library reports them (annety_crc_last_kernels)
         from annety_amd import _lib
 
         self._fixed = _lib.get().annety_crc32_batch_fixed
@@ -252,9 +246,13 @@ class Workload:
                                  self.out.data_ptr() + 4 * lo, stream_handle)
                 if st:
                     _lib.check(st, "annety_crc32_batch_fixed")
+                if self.kernel is None:
+                    self.kernel = annety_amd.last_kernels()
             return self.out[lo:hi]
         annety_amd.crc32_batch_var(self.data, self.offsets, self.lengths, out=self.out, stream=stream_handle,
                                    arena=True if self.arena else None)
+        if self.kernel is None:
+            self.kernel = annety_amd.last_kernels()
         return self.out
 
     def host_sample(self, max_bytes=4 << 20):
@@ -354,8 +352,9 @@ def cpu_baseline(h: np.ndarray, offs: np.ndarray, lens: np.ndarray, budget_s: fl
         "kind": kind,
         "compile_flags": REF_FLAGS if kind == "reference" else "gcc -O2 (oracle/Makefile, C restatement)",
         "single_thread_value": round(st_rate, 3),
-        "sample": f"{n} payloads / {nbytes / 2**20:.1f} MiB prefix of the GPU workload copied to host, crc32_long "
-                  f"per payload, payload-parallel over {threads} threads x {mt_reps} passes (+ 1 thread x {st_reps})",
+        "sample": f"{n} payloads / {nbytes / 2**20:.1f} MiB prefix of the GPU workload copied to host (memory-resident, "
+                  f"far above the host caches), crc32_long per payload, payload-parallel over {threads} threads x "
+                  f"{mt_reps} passes (+ 1 thread x {st_reps})",
     }
 
 
@@ -376,7 +375,7 @@ def pmc_traffic(w: Workload, var_path: str):
         return None
     if w.config == 4:  # the config-1 measurement is per 1M payloads; a config-4 step is n/1M of them
         tot = int(tot * w.n / (1 << 20))
-    return tot
+    return tot, path
 
 
 def e2e_host_path(w: Workload):
@@ -533,6 +532,7 @@ def main():
     torch.cuda.synchronize()
     hs, ho, hl = w.host_sample()
     want = oracle.batch_var(hs, ho, hl)
+    steady_kernels = w.kernel
     got = w.out[: len(ho)].cpu().numpy().view(np.uint32)
     if not np.array_equal(got, want):
         raise SystemExit(f"rank {rank}: digests differ from the oracle on the sample")
@@ -588,6 +588,12 @@ def main():
     ngroups = len(per_step)
 
     if rank == 0:
+        traffic = pmc_traffic(w, args.var_path)
+        cpu = None
+        if not (args.no_cpu or multi):
+            cs, co, cl = w.host_sample(CPU_SAMPLE_BYTES)
+            cpu = cpu_baseline(cs, co, cl, args.cpu_seconds)
+            del cs
         # every rank's payload bytes (weak: n per GPU x world; strong: the fixed total)
         total_gib = (w.n_total * w.L if w.L else w.payload_bytes * world) * args.steps / 2 ** 30
         achieved = w.algo_bytes / (kern_ms / 1e3) / 1e9
@@ -630,14 +636,17 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": pmc_traffic(w, args.var_path),
-                "kernel": w.kernel,
+                "traffic": traffic[0] if traffic else None,
+                "traffic_source": (f"{traffic[1]}: rocprofv3 PMC pass (FETCH_SIZE x2 + WRITE_SIZE) of this command, "
+                                   "committed" if traffic else None),
+                "kernel": steady_kernels,
+                "kernel_source": "annety_crc_last_kernels() after the gate's step (the library's own launch choice)",
                 "kernel_ms_avg": round(kern_ms, 4),
                 "kernel_ms_median": round(kern_median, 4),
                 "timing_groups": ngroups,
                 "algorithmic_bytes_per_launch": w.algo_bytes,
             },
-            "cpu_baseline": None if (args.no_cpu or multi) else cpu_baseline(hs, ho, hl, args.cpu_seconds),
+            "cpu_baseline": cpu,
             "checked_vs_oracle": checked,
         }
         if multi:

@@ -20,10 +20,18 @@
  * Streams: the variable, arena and split paths keep per-call device scratch per (device, stream), reused
  * in stream order with no per-call event and no host wait (hipStreamPerThread is keyed per calling
  * thread, since that handle names a different stream in every thread). Up to 64 streams per device
- * (ANNETY_CRC_STREAM_SLOTS) hold their own; past that, the least recently used stream's scratch is
- * handed over by an event recorded on that stream and waited by the new one (no device-wide sync, no
- * host block). A stream that has used these paths must stay valid until annety_crc_stream_release(stream)
- * (or annety_crc_shutdown): call it before hipStreamDestroy.
+ * (ANNETY_CRC_STREAM_SLOTS) hold their own. While all 64 are taken, every call records an event on its own
+ * stream right after its work, and a new stream takes the least recently used scratch over by waiting for
+ * that event; a scratch whose last call predates the table filling up is taken over after one device-wide
+ * synchronisation instead. The library never records on, or waits for, a stream other than the calling
+ * one, so a stream destroyed without annety_crc_stream_release is harmless; releasing it (before
+ * hipStreamDestroy) returns its scratch at once and avoids that synchronisation. A new stream whose handle
+ * value equals a destroyed one's takes that scratch over in its own order (hipStreamDestroy has completed
+ * the old stream's work by then).
+ * Failures: annety_crc_last_hip_error names the HIP error and annety_crc_last_error_stage the step of the
+ * host path that saw it (per thread). Work queued on a stream reports its failure at the next synchronising
+ * call; with ANNETY_CRC_SYNC_STAGES=1 the host-memory paths synchronise after every step so that the stage
+ * named is the one that failed (a diagnostic mode, slower).
  */
 #ifndef ANNETY_CRC_H
 #define ANNETY_CRC_H
@@ -35,7 +43,7 @@
 extern "C" {
 #endif
 
-#define ANNETY_CRC_ABI_VERSION 3
+#define ANNETY_CRC_ABI_VERSION 4
 
 enum {
   ANNETY_CRC_OK = 0,
@@ -56,6 +64,13 @@ int annety_crc_shutdown(void);
 const char* annety_crc_strerror(int status);
 /* Last hipError_t seen by this thread (0 if none). */
 int annety_crc_last_hip_error(void);
+/* The host-path step ("upload (packed)", "arena verify", "final sync", ...) of this thread's last HIP
+ * failure ("" if none). Static string. */
+const char* annety_crc_last_error_stage(void);
+/* The kernels this thread's latest device entry point enqueued, in launch order, joined by " + " (e.g.
+ * "crc32_onekib_nt_kernel" for BASELINE config 1, "crc32_arena_lines_kernel + crc32_arena_stitch_kernel" for
+ * an arena batch). Valid until the thread's next call; "" before any. */
+const char* annety_crc_last_kernels(void);
 /* Leave n CUs of every device free of the batch kernels (which otherwise take one workgroup per CU), so
  * that work on other streams - e.g. the RCCL kernels of a digest gather overlapped with the next chunk -
  * runs beside them instead of between them. 0 (default) uses every CU. Process-wide. */
@@ -104,12 +119,16 @@ const uint32_t* annety_crc32_table256(void);
 int annety_crc32_batch_fixed(const void* d_base, size_t n, size_t len, size_t stride, uint32_t* d_out,
                              void* stream);
 /* Variable length: payload i = [d_base + d_off[i], + d_len[i]) (any alignment).
- * Path choice is automatic: every call also records the batch's extent on the device (a few us), and once
- * two completed calls on the same stream with the same (d_base, d_off, d_len, n) have shown a dense, sorted
- * batch (starts ascending, gaps < 4 KiB, payload bytes >= 2/3 of the span) the call runs the arena path over
- * that span; otherwise (and for n < 1024) the length-sorted path. The arena launches re-check the call's
- * own extent on the device, so a batch whose layout changed under the same pointers is still exact (its
- * payloads are then folded directly, more slowly, for that call). ANNETY_CRC_VAR_AUTO=0: sorted path only. */
+ * Path choice is automatic. A recording call runs the extent kernel (a few us), which publishes the batch's
+ * extent; once two completed recording calls on the same stream with the same (d_base, d_off, d_len, n) have
+ * shown a dense, sorted batch (starts ascending, gaps < 4 KiB, payload bytes >= 2/3 of the span), calls take
+ * the arena path over that span; otherwise (and for n < 1024) the length-sorted path. On the arena path one
+ * call in 8 records: it re-checks its own extent on the device and, if the layout changed under the same
+ * pointers, folds every payload directly from its own bytes. The 7 calls in between skip the extent kernel
+ * and the device check: the span is checked on the host to lie inside one device allocation (so the line
+ * pass reads only mapped memory), and the stitch folds any payload outside the span from its own bytes. In
+ * every call each digest depends only on its payload's bytes: a changed layout costs time, never a wrong
+ * digest or a read of unmapped memory. ANNETY_CRC_VAR_AUTO=0: sorted path only. */
 int annety_crc32_batch_var(const void* d_base, const uint64_t* d_off, const uint32_t* d_len, size_t n,
                            uint32_t* d_out, void* stream);
 /* Raw-register update (crc32_update semantics) for a fixed-length batch: d_state[i] is the register
@@ -140,7 +159,12 @@ int annety_crc32_update_batch_var_arena(uint32_t* d_state, const void* d_arena, 
  * Synchronous. ---- */
 int annety_crc32_batch_fixed_host(const void* h_base, size_t n, size_t len, size_t stride, uint32_t* h_out);
 /* Pin (hipHostRegister) / unpin a long-lived host buffer, e.g. a NetBuffer arena: host batches whose
- * payloads lie in pinned memory are copied to the device in place, without the staging pack. */
+ * payloads lie inside one buffer pinned here are copied to the device in place, without the staging pack.
+ * h_ptr must be page-aligned, and the buffer's pages must not overlap a buffer already pinned here
+ * (ANNETY_CRC_EINVAL otherwise): the runtime pins whole pages, and registrations sharing a page leave its
+ * lookup two answers. Only buffers pinned through this call are DMA'd in place; any other host memory
+ * (including memory pinned by other means) goes through the pack. unregister takes the same h_ptr
+ * (ANNETY_CRC_EINVAL for a pointer not pinned here). */
 int annety_crc_host_register(void* h_ptr, size_t bytes);
 int annety_crc_host_unregister(void* h_ptr);
 
@@ -222,6 +246,10 @@ int annety_lhc_verify_host(const void* h_stream, size_t size, int length_type, i
 int annety_lhc_verify_host_iov(const void* const* h_bufs, const size_t* sizes, size_t k, int length_type,
                                int64_t max_payload, uint64_t* h_payload_off, uint32_t* h_payload_len, uint8_t* h_ok,
                                size_t max_frames, size_t* conn_frames, size_t* conn_consumed, int* conn_rt);
+/* How annety_*_verify_host(_iov) uploads receive buffers that are not pinned here: 1 (default; initial value
+ * from ANNETY_CRC_FRAMES_PACK) packs them into the library's pinned ring with the pack threads, 0 hands them
+ * to the runtime's pageable copy. Process-wide; results do not depend on it. */
+int annety_crc_set_frames_pack(int pack);
 /* Host plan for a batch of LengthHeaderCodec::encode calls (:169-176): h_rt[i] (optional) = 1, or 0 for
  * an empty payload, or -1 for len > max_payload (max_payload > 0); h_frame_off[i] = where frame i starts
  * when the frames of accepted payloads are packed back to back (rejected ones take no bytes);

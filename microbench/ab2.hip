@@ -2,6 +2,7 @@
 // the single-round kernel (kVwg). Includes the product source directly.
 #include "../annety_amd/csrc/crc32_kernels.hip"
 #include "../annety_amd/csrc/crc32_frames.hip"
+#include "../annety_amd/csrc/crc32_host.cpp"
 #include "../annety_amd/csrc/crc32_capi.cpp"
 #include <cstdio>
 #include <vector>

@@ -4,6 +4,7 @@
 #include "../annety_amd/csrc/crc32_kernels.hip"
 #include "../annety_amd/csrc/crc32_arena.hip"
 #include "../annety_amd/csrc/crc32_frames.hip"
+#include "../annety_amd/csrc/crc32_host.cpp"
 #include "../annety_amd/csrc/crc32_capi.cpp"
 #include <cstdio>
 #include <vector>

@@ -221,6 +221,31 @@ def test_boundary_error_paths_without_device():
         assert lib.annety_crc_stream_release(None) < 0
 
 
+def test_host_register_refuses_shared_pages_without_device():
+    """annety_crc_host_register's argument rules run before any HIP call: a pointer that is not
+    page-aligned, zero bytes or null is refused with EINVAL, and unregistering a pointer the library did
+    not pin is EINVAL too (the library never passes such a pointer to the runtime). The overlap rule is
+    covered with real registrations in tests/test_gpu_parity.py and in the host self-test."""
+    import ctypes
+    import mmap
+
+    lib = _lib.get()
+    m = mmap.mmap(-1, 4 * mmap.PAGESIZE)
+    buf = (ctypes.c_uint8 * len(m)).from_buffer(m)
+    base = ctypes.addressof(buf)
+    assert base % mmap.PAGESIZE == 0
+    assert lib.annety_crc_host_register(base + 8, 100) == -1  # not page-aligned
+    assert lib.annety_crc_host_register(base, 0) == -1
+    assert lib.annety_crc_host_register(None, 100) == -1
+    assert lib.annety_crc_host_unregister(base) == -1  # not pinned here
+    assert lib.annety_crc_host_unregister(None) == -1
+    assert lib.annety_crc_last_error_stage() in (b"", None) or isinstance(lib.annety_crc_last_error_stage(), bytes)
+    assert lib.annety_crc_set_frames_pack(2) == -1
+    assert lib.annety_crc_set_frames_pack(1) == 0
+    del buf
+    m.close()
+
+
 def test_product_kernels_do_not_spill(tmp_path):
     """Every gfx950 kernel in libannety_crc.so runs without scratch (no VGPR spills): the 1024-lane stitch
     variant that returned wrong digests in round 2 was the only build that spilled (DESIGN.md §7.2;

@@ -1,7 +1,9 @@
-"""Per-call scratch across streams (crc32_capi.cpp scratch_slot: arena, sorted and split paths): each
-stream keeps its own scratch slot, fenced by stream order; past the slot cap (ANNETY_CRC_STREAM_SLOTS,
-default 64) the least recently used slot is handed over by an event recorded on its last stream - never
-a device-wide synchronise (annety_crc_scratch_stats counts them). Streams interleave arena batches of
+"""Per-call scratch across streams (crc32_host.h SlotTable: arena, sorted and split paths): each stream
+keeps its own scratch slot, fenced by stream order; past the slot cap (ANNETY_CRC_STREAM_SLOTS, default 64)
+the least recently used slot is handed over - by the event its last call recorded on its own stream while
+the table was full, or after one device-wide synchronise for a slot last used before the table filled up
+(annety_crc_scratch_stats counts both). No event is ever recorded on a stream other than the caller's, so
+streams destroyed without annety_crc_stream_release are harmless. Streams interleave arena batches of
 different sizes, several rounds each, and every digest is compared with the oracle. Batches are packed
 Zipf-like lengths at unaligned starts, so every call runs the line pass and the stitch (the path of
 BASELINE config 3). hipStreamPerThread, one handle naming a different stream per thread, gets a slot
@@ -182,7 +184,8 @@ print("RESULT", bad, s["slots"], s["handoffs"], s["device_syncs"])
 
 def test_slot_handoff_past_the_cap(gpu, tmp_path):
     """With the cap at 4 slots, 11 streams x 3 rounds take slots over from each other: every digest is
-    right, hand-overs happen, and none of them synchronises the device."""
+    right, hand-overs happen, and only the first one (of a slot last used before the table was full)
+    synchronises the device."""
     import os
     import subprocess
     import sys
@@ -194,7 +197,91 @@ def test_slot_handoff_past_the_cap(gpu, tmp_path):
     r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=110, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     bad, slots, handoffs, syncs = map(int, [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT")][0].split()[1:])
-    assert bad == 0 and slots == 4 and handoffs > 0 and syncs == 0
+    assert bad == 0 and slots == 4 and handoffs > 0 and syncs == 1
+
+
+DEAD_STREAMS_SCRIPT = r"""
+import ctypes
+import sys
+import numpy as np
+import torch
+sys.path.insert(0, {root!r})
+sys.path.insert(0, {tests!r})
+import annety_amd
+import oracle
+import test_gpu_arena_streams as t
+from annety_amd import sharded
+hip = ctypes.CDLL("libamdhip64.so")
+gpu = torch.device("cuda", 0)
+d, o, ln, want, nb = t._arena_job(gpu, 77, (1 << 20) + 4321)
+n, L = 3, (1 << 20) + 4096  # a few long payloads: the split path (a scratch slot too)
+lb = np.random.default_rng(5).integers(0, 256, n * L, dtype=np.uint8)
+lwant = oracle.batch_fixed(lb, n, L)
+ld = torch.from_numpy(lb).to(gpu)
+torch.cuda.synchronize()
+bad = 0
+# 12 raw HIP streams alive at once (distinct handles), each used by the arena and the split path, then all
+# destroyed WITHOUT annety_crc_stream_release: the slot table (cap 4) hands slots over among them and must
+# never touch a dead handle afterwards
+raw = []
+for i in range(12):
+    s = ctypes.c_void_p()
+    assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+    raw.append(s)
+for rnd in range(2):
+    for s in raw:
+        out = torch.empty(ln.numel(), dtype=torch.int32, device=gpu)
+        lout = torch.empty(n, dtype=torch.int32, device=gpu)
+        annety_amd.crc32_batch_var(d, o, ln, out=out, stream=s.value, arena=nb)
+        annety_amd.crc32_batch(ld, n, L, out=lout, stream=s.value)
+        assert hip.hipStreamSynchronize(s) == 0
+        bad += int((out.cpu().numpy().view(np.uint32) != want).sum()) + int((lout.cpu().numpy().view(np.uint32) != lwant).sum())
+for s in raw:
+    assert hip.hipStreamDestroy(s) == 0
+# new streams after the old ones died (HIP may hand out the dead handles' values again: hipStreamDestroy has
+# finished their work, so a reused value takes its slot over in stream order)
+for i in range(6):
+    s = ctypes.c_void_p()
+    assert hip.hipStreamCreate(ctypes.byref(s)) == 0
+    out = torch.empty(ln.numel(), dtype=torch.int32, device=gpu)
+    annety_amd.crc32_batch_var(d, o, ln, out=out, stream=s.value, arena=nb)
+    assert hip.hipStreamSynchronize(s) == 0
+    bad += int((out.cpu().numpy().view(np.uint32) != want).sum())
+    assert hip.hipStreamDestroy(s) == 0
+# device groups created and destroyed past the cap (their compute streams run the split path)
+for i in range(6):
+    with sharded.DeviceGroup([0]) as g:
+        out = g.batch_fixed([ld], L, chunks=1)
+        torch.cuda.synchronize()
+        bad += int((out.cpu().numpy().view(np.uint32) != lwant).sum())
+# then a call on a fresh stream
+s2 = torch.cuda.Stream(gpu)
+out = torch.empty(ln.numel(), dtype=torch.int32, device=gpu)
+annety_amd.crc32_batch_var(d, o, ln, out=out, stream=s2, arena=nb)
+torch.cuda.synchronize()
+bad += int((out.cpu().numpy().view(np.uint32) != want).sum())
+st = annety_amd.scratch_stats(0)
+print("RESULT", bad, st["slots"], st["handoffs"], st["device_syncs"])
+"""
+
+
+def test_destroyed_streams_past_the_cap(gpu, tmp_path):
+    """Streams destroyed without annety_crc_stream_release, more of them than slots (cap 4), and device
+    groups created and destroyed past the cap: every digest is right, the process ends cleanly (no event
+    recorded on a dead stream), the groups released their streams' slots (the table stays at the cap), and
+    the dead streams' slots are taken over with at most one device synchronise per table fill."""
+    import os
+    import subprocess
+    import sys
+
+    here = os.path.dirname(os.path.abspath(__file__))
+    script = tmp_path / "dead_streams.py"
+    script.write_text(DEAD_STREAMS_SCRIPT.format(root=os.path.dirname(here), tests=here))
+    env = dict(os.environ, ANNETY_CRC_STREAM_SLOTS="4")
+    r = subprocess.run([sys.executable, str(script)], capture_output=True, text=True, timeout=110, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    bad, slots, handoffs, syncs = map(int, [ln for ln in r.stdout.splitlines() if ln.startswith("RESULT")][0].split()[1:])
+    assert bad == 0 and slots <= 4 and handoffs > 0 and syncs <= 2
 
 
 def test_per_thread_stream_handle_two_threads(gpu):

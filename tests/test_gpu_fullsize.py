@@ -1,9 +1,10 @@
-"""Full-size parity at the BASELINE shapes the bench runs (configs 2 and 3), through the C-ABI.
+"""Full-size parity at every BASELINE shape the bench runs (configs 1-4), through the C-ABI.
 
+Config 1: 1M x 1 KiB (1 GiB), every digest (tests/test_gpu_parity.py::test_config1_full_bitexact). Config 2: 4096 x 4 MiB = 16 GiB resident, every digest.
 Config 3: the bench's own Zipf batch (~164k payloads, 1 GiB, packed back-to-back so starts are
-unaligned), digests AND crc32_update registers compared bit-exactly with the multi-threaded oracle
-on every payload. Config 2: 4096 x 4 MiB = 16 GiB resident, compared on every payload.
-Each test prints its progress so a stall names its stage.
+unaligned), digests AND crc32_update registers on every payload, both variable paths. Config 4: one
+GPU's shard, 8M x 1 KiB = 8 GiB, checksummed in the bench's chunks, every digest. All compared
+bit-exactly with the multi-threaded oracle. Each test prints its progress so a stall names its stage.
 """
 import os
 import sys
@@ -90,3 +91,36 @@ def test_config2_full_bitexact(gpu):
     want = oracle.batch_fixed_mt(host, n, L, threads=THREADS)
     bad = np.nonzero(got != want)[0]
     assert bad.size == 0, f"{bad.size} mismatches, first {bad[:8]}"
+
+
+def _check_fixed_pieces(data, got, n, L, tag):
+    """Every digest against the oracle, 1 GiB of payloads at a time (host memory stays bounded)."""
+    per = (1 << 30) // L
+    for lo in range(0, n, per):
+        hi = min(n, lo + per)
+        host = data[lo * L:hi * L].cpu().numpy()
+        want = oracle.batch_fixed_mt(host, hi - lo, L, threads=THREADS)
+        bad = np.nonzero(got[lo:hi] != want)[0]
+        assert bad.size == 0, f"{tag}: {bad.size} mismatches in payloads [{lo}, {hi}), first {bad[:8] + lo}"
+
+
+def test_config4_shard_full(gpu):
+    """BASELINE config 4's per-GPU shard: 8M x 1 KiB (8 GiB) resident, checksummed in the bench's two
+    chunks (bench.py --config 4: annety_crc32_batch_fixed per chunk), every digest against the oracle."""
+    import torch
+
+    from annety_amd import _lib
+
+    n, L, chunks = 8 << 20, 1024, 2
+    g = torch.Generator(device=gpu)
+    g.manual_seed(4444)
+    data = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=gpu, generator=g)
+    out = torch.zeros(n, dtype=torch.int32, device=gpu)
+    sh = int(torch.cuda.current_stream(gpu).cuda_stream)
+    for c in range(chunks):
+        lo, hi = n * c // chunks, n * (c + 1) // chunks
+        _lib.check(_lib.get().annety_crc32_batch_fixed(data.data_ptr() + lo * L, hi - lo, L, L,
+                                                        out.data_ptr() + 4 * lo, sh), "annety_crc32_batch_fixed")
+    got = _u32(out)
+    print("config 4 shard: 8 GiB digests done", flush=True)
+    _check_fixed_pieces(data, got, n, L, "config 4 shard")

@@ -191,6 +191,7 @@ def test_config1_full_bitexact(config1):
 
     n, L, data = config1
     got = digests(annety_amd.crc32_batch(data, n, L))
+    assert annety_amd.last_kernels() == "crc32_onekib_nt_kernel"  # the kernel bench.py's roofline names
     host = data.cpu().numpy()
     want = oracle.batch_fixed_mt(host, n, L, threads=16)
     bad = np.nonzero(got != want)[0]
@@ -281,3 +282,42 @@ def test_update_batch_fixed_odd_shapes(gpu):
         annety_amd.crc32_update_batch(d_state, d[off:], n, L, stride)
         want = [oracle.crc32_update(int(states[i]), host[off + i * stride : off + i * stride + L]) for i in range(n)]
         assert [int(x) for x in digests(d_state)] == want, (n, L, stride, off)
+
+
+def test_host_registrations(gpu):
+    """annety_crc_host_register: page-aligned ranges only, no two sharing a page; only buffers pinned here
+    are DMA'd in place, anything else (a view that leaves the pinned range, memory after unregister) goes
+    through the pack - the digests are the same either way."""
+    import ctypes
+    import mmap
+
+    import annety_amd
+    from annety_amd import _lib
+
+    lib = _lib.get()
+    pg = mmap.PAGESIZE
+    m = mmap.mmap(-1, 8 * pg)
+    buf = np.frombuffer(m, dtype=np.uint8)
+    buf[:] = oracle.lcg_bytes(buf.size, 91)
+    base = buf.ctypes.data
+    assert lib.annety_crc_host_register(base, 2 * pg + 100) == 0
+    assert lib.annety_crc_host_register(base + 2 * pg, pg) == -1  # shares the first range's last page
+    assert lib.annety_crc_host_register(base + pg, pg) == -1       # inside it
+    assert lib.annety_crc_host_register(base + 3 * pg, 2 * pg) == 0
+    assert lib.annety_crc_host_unregister(base + pg) == -1         # not a range start
+    n, L = 40, 64
+    want = oracle.batch_fixed(buf, n, L)
+    assert np.array_equal(annety_amd.crc32_batch_host(buf[: n * L], n, L), want)  # inside range 1: in place
+    want2 = oracle.batch_fixed(buf[2 * pg:], 100, 64)
+    assert np.array_equal(annety_amd.crc32_batch_host(buf[2 * pg: 2 * pg + 6400], 100, 64), want2)  # spans both
+    assert lib.annety_crc_host_unregister(base) == 0
+    assert lib.annety_crc_host_unregister(base + 3 * pg) == 0
+    assert lib.annety_crc_host_unregister(base) == -1
+    assert np.array_equal(annety_amd.crc32_batch_host(buf[: n * L], n, L), want)
+    p = annety_amd.PinnedHostBuffer(3 * pg + 5)
+    assert p.array.ctypes.data % pg == 0 and p.array.size == 3 * pg + 5
+    p.array[:] = buf[: p.array.size]
+    assert np.array_equal(annety_amd.crc32_batch_host(p.array, n, L), want)
+    p.close()
+    del buf
+    m.close()

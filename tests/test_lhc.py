@@ -130,7 +130,7 @@ def test_gpu_decode_host_large_stream(gpu):
     import annety_amd
 
     rng = np.random.default_rng(9)
-    lens = np.minimum(65536, 64 * rng.zipf(1.3, 6000) + rng.integers(0, 64, 6000)).astype(np.int64)
+    lens = np.minimum(65536, 64 * np.minimum(rng.zipf(1.3, 6000), 1 << 20) + rng.integers(0, 64, 6000)).astype(np.int64)
     body = oracle.lcg_bytes(int(lens.sum()), 31)
     pieces, pos = [], 0
     for L in lens.tolist():
@@ -402,12 +402,24 @@ def test_property_plan_equals_sequential_encode(lens, T, maxp):
     assert total == pos
 
 
+@pytest.fixture(params=[True, False], ids=["pack", "pageable"])
+def frames_pack(request, gpu):
+    """Both upload modes of the frame paths for buffers not pinned here: packed into the library's pinned
+    ring (the default) and handed to the runtime's pageable copy (annety_crc_set_frames_pack)."""
+    import annety_amd
+
+    annety_amd.set_frames_pack(request.param)
+    yield request.param
+    annety_amd.set_frames_pack(True)
+
+
 @pytest.mark.gpu
-def test_gpu_decode_host_iov_replays_every_recorded_stream(golden, gpu):
+def test_gpu_decode_host_iov_replays_every_recorded_stream(golden, frames_pack):
     """annety_lhc_verify_host_iov: the reference codec's 95 recorded decode streams as 95 connections'
     receive buffers, one call per codec configuration (T, max_payload) - all 95 in as many calls as there
     are configurations, 93 of them in the four largest calls - each connection's frames, consumed bytes
-    and rt equal to the reference's Codec::recv sequence. Then the same with the buffers pinned."""
+    and rt equal to the reference's Codec::recv sequence. Then the same with the buffers pinned
+    (page-aligned registrations of their own pages, PinnedHostBuffer)."""
     import annety_amd
 
     groups = {}
@@ -436,7 +448,7 @@ def test_gpu_decode_host_iov_replays_every_recorded_stream(golden, gpu):
 
 
 @pytest.mark.gpu
-def test_gpu_decode_host_iov_large(gpu):
+def test_gpu_decode_host_iov_large(frames_pack):
     """Many connections whose buffers cross the 64 MiB staging chunks (frames and headers straddle chunk
     boundaries, the walk follows the pack), with corrupted frames and ragged tails: every connection's
     verdicts equal the single-stream path's and the oracle's."""
@@ -445,7 +457,8 @@ def test_gpu_decode_host_iov_large(gpu):
     bufs, want = [], []
     for conn in range(40):
         n = int(rng.integers(0, 900))
-        lens = np.minimum(65536, 64 * rng.zipf(1.3, n) + rng.integers(0, 64, n)).astype(np.int64) if n else []
+        lens = (np.minimum(65536, 64 * np.minimum(rng.zipf(1.3, n), 1 << 20) + rng.integers(0, 64, n)).astype(np.int64)
+                if n else [])
         body = oracle.lcg_bytes(int(np.sum(lens)) if n else 0, 500 + conn)
         out, pos, starts = [], 0, []
         for L in (lens.tolist() if n else []):
