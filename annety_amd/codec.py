@@ -70,14 +70,20 @@ def recv_result(length_type: int, off: np.ndarray, ln: np.ndarray, used: int, in
 
 
 _scratch = threading.local()
+# Largest bound whose arrays a thread keeps between calls: 16M frames (208 MB), above the first bound of a
+# 1 GiB stream (_frame_caps: ~8.4M). A worst-case retry (a frame per T + 4 bytes: 134M frames, 1.7 GB for
+# 1 GiB) gets arrays of its own that go with the call.
+_CACHE_MAX_FRAMES = 16 << 20
 
 
 def _out_arrays(cap: int):
-    """This thread's output arrays for a frame walk of at most `cap` frames (grow-only, reused by every
-    call; the results are copied out of them). Arrays of the bound's size allocated per call cost more than
-    the verify itself on a 1 GiB stream: 110 MB of them, 28 GiB/s against 51 with arrays of the exact frame
-    count."""
+    """This thread's output arrays for a frame walk of at most `cap` frames (grow-only up to
+    _CACHE_MAX_FRAMES, reused by every call; the results are copied out of them). Arrays of the bound's size
+    allocated per call cost more than the verify itself on a 1 GiB stream: 110 MB of them, 28 GiB/s against
+    51 with arrays of the exact frame count."""
     c = max(int(cap), 1)
+    if c > _CACHE_MAX_FRAMES:
+        return np.empty(c, np.uint64), np.empty(c, np.uint32), np.empty(c, np.uint8)
     have = getattr(_scratch, "arrays", None)
     if have is None or have[0].size < c:
         have = (np.empty(c, np.uint64), np.empty(c, np.uint32), np.empty(c, np.uint8))

@@ -88,7 +88,8 @@ class PipelinedGather:
         self.bounds = chunk_bounds(n_local, chunks, taper)
         # one receive buffer per digest buffer (run_steps): gathers in flight together never share one, so
         # the result does not depend on the backend running them in order (gloo runs them on a thread pool)
-        self.recvs = ([torch.empty((self.world, n_local), dtype=dtype, device=device) for _ in range(max(1, buffers))]
+        self.buffers = max(1, buffers)
+        self.recvs = ([torch.empty((self.world, n_local), dtype=dtype, device=device) for _ in range(self.buffers)]
                       if self.rank == dst else None)
         self.last = 0  # the receive buffer of the latest step
 
@@ -114,16 +115,20 @@ class PipelinedGather:
         for h in handles:
             h.wait()
 
-    def run_steps(self, produce: Callable[[int, int, int], torch.Tensor], steps: int, buffers: int = 2,
+    def run_steps(self, produce: Callable[[int, int, int], torch.Tensor], steps: int, buffers: Optional[int] = None,
                   gather: bool = True) -> None:
         """`steps` consecutive steps; produce(s, lo, hi) writes step s's digests of [lo, hi) into buffer
         s % buffers and returns that view. Step s's handles are waited (on a GPU: the compute stream waits
         for step s's gathers, no host block) only after step s + buffers - 1 is launched, just before step
         s + buffers reuses the buffer: with two buffers step s+1 computes while step s's last gathers still
-        read the other one. Everything is waited before returning."""
+        read the other one. Everything is waited before returning. `buffers` defaults to the receive buffers
+        allocated at construction; more would put two steps' gathers in flight into one receive buffer."""
         from collections import deque
 
-        buffers = max(1, buffers)
+        buffers = self.buffers if buffers is None else max(1, buffers)
+        if buffers > self.buffers:
+            raise ValueError(f"run_steps with {buffers} buffers, but the gather was built with {self.buffers} "
+                             "receive buffers (PipelinedGather(buffers=...))")
         pending = deque()
         for s in range(steps):
             pending.append(self.run(lambda lo, hi, s=s: produce(s, lo, hi), gather=gather, buf=s % buffers))

@@ -150,9 +150,14 @@ def _steps_worker(rank, world, port, n_local, L, chunks, steps, buffers, q):
             out[lo:hi] = torch.from_numpy(oracle.batch_fixed(arena[lo * L:hi * L], hi - lo, L).view(np.int32).copy())
             return out[lo:hi]
 
-        pipe.run_steps(produce, steps, buffers=buffers)
+        pipe.run_steps(produce, steps)  # defaults to the receive buffers built (never more)
         if rank == 0:
             q.put(("recv", pipe.recv.numpy().view(np.uint32).tolist()))
+        try:  # more digest buffers than receive buffers would share one receive buffer between steps
+            pipe.run_steps(produce, 1, buffers=buffers + 1)
+            q.put(("raise", rank, False))
+        except ValueError:
+            q.put(("raise", rank, True))
         # every buffer still holds its last step's digests (no step overwrote a buffer under a gather)
         for b in range(buffers):
             s = max(x for x in range(steps) if x % buffers == b)
@@ -175,8 +180,9 @@ def test_gloo_world2_run_steps(buffers):
     for p in procs:
         p.join(120)
         assert p.exitcode == 0
-    msgs = [q.get(timeout=5) for _ in range(1 + 2 * buffers)]
+    msgs = [q.get(timeout=5) for _ in range(3 + 2 * buffers)]
     assert all(m[3] for m in msgs if m[0] == "buf")
+    assert [m[2] for m in msgs if m[0] == "raise"] == [True, True]
     recv = [m for m in msgs if m[0] == "recv"][0][1]
     for r in range(2):  # rank 0 ends holding the last step's digests of every rank
         want = oracle.batch_fixed(oracle.lcg_bytes(n_local * L, 100 * (steps - 1) + r), n_local, L).tolist()
