@@ -101,9 +101,11 @@ def get() -> ctypes.CDLL:
         # running the host-side tests (frame walks, encode plans, shard plans) under ASan/UBSan or TSan; it
         # exports the host entry points only, so the device ones stay unbound and any call to them fails.
         host_only = os.environ.get("ANNETY_CRC_HOST_LIB")
-        if not host_only and not os.path.exists(_build.LIB):
+        # ANNETY_CRC_LIB: another full build of the library (same-box A/B against a baseline commit's build)
+        path = host_only or os.environ.get("ANNETY_CRC_LIB") or _build.LIB
+        if path == _build.LIB and not os.path.exists(_build.LIB):
             _build.build()  # raises if hipcc is unavailable: no silent fallback
-        lib = ctypes.CDLL(host_only or _build.LIB)
+        lib = ctypes.CDLL(path)
         for name, res, args in SIGNATURES:
             if host_only and not hasattr(lib, name):
                 continue
