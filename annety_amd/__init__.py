@@ -32,6 +32,7 @@ from .crc32c import (  # noqa: F401
     set_split,
     set_walk_segment,
     stream_release,
+    set_var_path,
     var_path_stats,
     tables,
 )
@@ -56,6 +57,7 @@ __all__ = [
     "set_split",
     "set_walk_segment",
     "stream_release",
+    "set_var_path",
     "var_path_stats",
     "tables",
     "LengthHeaderCodec",

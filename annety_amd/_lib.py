@@ -28,6 +28,8 @@ SIGNATURES = [
     ("annety_crc_set_split", ctypes.c_int, [ctypes.c_int, _u64]),
     ("annety_crc_set_walk_segment", ctypes.c_int, [_u64]),
     ("annety_crc_stream_release", ctypes.c_int, [_vp]),
+    ("annety_crc_set_var_path", ctypes.c_int, [ctypes.c_int]),
+    ("annety_crc_get_var_path", ctypes.c_int, []),
     ("annety_crc_var_path_stats", ctypes.c_int,
      [ctypes.c_int, ctypes.POINTER(_u64), ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
     ("annety_crc_scratch_stats", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_u64), ctypes.POINTER(_u64),

@@ -47,18 +47,7 @@ namespace {
 // register-pressure-dependent fault we did not pin down)
 constexpr int kStitchBlock = 512;
 
-// Map i of a set of T nibble-table maps stored [k][i][v] (k nibble position, v value): for one k the
-// set's tables lie side by side, so lanes applying different maps spread over the banks
-// ((16 i + v) mod 64) instead of all sharing the same 16 (a [i][k][v] layout cost the segment steps
-// up to 8-way conflicts).
-template <uint32_t T>
-__device__ __forceinline__ uint32_t nibble_map_set(uint32_t s, const uint32_t* lds, uint32_t off, uint32_t i) {
-  const uint32_t* t = lds + off / 4 + i * 16;
-  uint32_t r[8];
-#pragma unroll
-  for (int k = 0; k < 8; k++) r[k] = t[k * T * 16 + __builtin_amdgcn_ubfe(s, 4 * k, 4)];
-  return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6] ^ r[7]);
-}
+// (nibble_map_set: crc32_device.h)
 // ADJ: where the image starts in the full stitch layout (0, or kLdsHalfOff for the lite image, which
 // drops the slicing tables: see crc32_arena_stitch_lite_kernel).
 // shift_{-m} for m in [0, 128): U_hi[m >> 4] o U_lo[m & 15]

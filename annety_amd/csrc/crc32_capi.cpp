@@ -83,12 +83,20 @@ struct HostImages {
   std::vector<uint32_t> unshift; // 24 maps x 128 words (U_lo[0..15], U_hi[0..7])
   std::vector<uint32_t> sb;      // arena superblock join: (k, v, g) = shift_{(7-g)*1024}(v << 4k); byte map
   std::vector<uint32_t> stitch;  // arena stitch: segment maps F/G/UL/UB, unshift, shift_32 (crc32_math.h)
+  std::vector<uint32_t> stream;  // line-stream path: scan maps, U sets, power maps (crc32_math.h)
 };
 
 // Apply matrix m to (v << 4k) for every nibble value: the 16-entry table of one nibble position.
 void nibble_tables(const Gf2Mat& m, uint32_t* out /* [8][16] */) {
   for (int kk = 0; kk < 8; kk++)
     for (uint32_t v = 0; v < 16; v++) out[kk * 16 + v] = gf2_apply(m, v << (4 * kk));
+}
+
+// A set of T maps stored [k][i][v] (crc32_device.h nibble_map_set) from maps stored [i][k][v].
+void put_set(uint32_t* dst, const uint32_t* maps, uint32_t T) {
+  for (uint32_t i = 0; i < T; i++)
+    for (uint32_t kk = 0; kk < 8; kk++)
+      for (uint32_t v = 0; v < 16; v++) dst[(kk * T + i) * 16 + v] = maps[i * 128 + kk * 16 + v];
 }
 
 Gf2Mat gf2_inverse(const Gf2Mat& m) {
@@ -182,12 +190,6 @@ const HostImages& host_images() {
     }
     img.stitch.assign((kLdsStitchImageBytes - kLdsCommonBytes) / 4, 0);
     {
-      // sets of maps stored [k][i][v] (crc32_arena.hip nibble_map_set)
-      auto put_set = [](uint32_t* dst, const uint32_t* maps /* [i][k][v] */, uint32_t T) {
-        for (uint32_t i = 0; i < T; i++)
-          for (uint32_t kk = 0; kk < 8; kk++)
-            for (uint32_t v = 0; v < 16; v++) dst[(kk * T + i) * 16 + v] = maps[i * 128 + kk * 16 + v];
-      };
       std::vector<uint32_t> seg(32 * 128);
       const Gf2Mat inv128 = gf2_inverse(shift_matrix(128)), inv1024 = gf2_inverse(shift_matrix(1024));
       Gf2Mat ul{}, ub{};
@@ -205,6 +207,14 @@ const HostImages& host_images() {
       put_set(m + (kLdsStitchUnshiftOff - kLdsMapOff) / 4, img.unshift.data(), 16);                  // U_lo
       put_set(m + (kLdsStitchUnshiftOff + 8192 - kLdsMapOff) / 4, img.unshift.data() + 16 * 128, 8);  // U_hi
       nibble_tables(shift_matrix(32), m + (kLdsQuarterOff - kLdsMapOff) / 4);
+    }
+    img.stream.assign(kStreamFixupBytes / 4, 0);
+    {
+      uint32_t* m = img.stream.data();
+      for (uint32_t i = 0; i < 6; i++) nibble_tables(shift_matrix((uint64_t)kChunkBytes << i), m + (kStreamScanOff + 512 * i) / 4);
+      put_set(m + kStreamULoOff / 4, img.unshift.data(), 16);
+      put_set(m + kStreamUHiOff / 4, img.unshift.data() + 16 * 128, 8);
+      for (uint32_t i = 0; i < 32; i++) nibble_tables(shift_matrix((uint64_t)kChunkBytes << i), m + (kStreamPowOff + 512 * i) / 4);
     }
   });
   return img;
@@ -254,6 +264,13 @@ struct Scratch {
   uint64_t since_extent = 0;              // arena calls since the last one that recorded its extent
   uint64_t seen_seq = 0, prev_seq = 0;    // the two latest completed hints read for this key
   ExtentHint seen{}, prev{};
+  // line-stream path (run_var_stream): the scan's two look-back status sets, alternating per call; each call
+  // zeroes the records the previous one left in the other set
+  uint64_t* st = nullptr;  // 2 sets of st_set_words words
+  size_t st_set_words = 0;
+  uint64_t st_calls = 0;            // set (st_calls & 1) is the next call's
+  uint32_t st_used[2] = {0, 0};     // tiles the latest call on each set wrote (0: the set is zero)
+  bool st_clean = false;            // both sets zero (false after an allocation or a failed launch)
 };
 using ScratchSlot = host::Slot<Scratch>;
 
@@ -300,6 +317,7 @@ struct DeviceCtx {
   uint32_t* d_unshift = nullptr;
   void* d_sb = nullptr;
   void* d_stitch = nullptr;
+  void* d_stream_img = nullptr;
   void* d_zero = nullptr;  // 256 zero bytes
   Staging stg;
   std::mutex stg_mu;  // one host-staged batch at a time per device
@@ -324,12 +342,12 @@ size_t grid_cus(const DeviceCtx& c) { return (size_t)std::max(1, c.cus - g_reser
 std::mutex g_init_mu;
 
 void free_images(DeviceCtx& c) {
-  void* bufs[] = {c.d_slice, c.d_groups, c.d_unshift, c.d_sb, c.d_stitch, c.d_zero};
+  void* bufs[] = {c.d_slice, c.d_groups, c.d_unshift, c.d_sb, c.d_stitch, c.d_stream_img, c.d_zero};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   c.d_slice = c.d_groups = nullptr;
   c.d_unshift = nullptr;
-  c.d_sb = c.d_stitch = c.d_zero = nullptr;
+  c.d_sb = c.d_stitch = c.d_stream_img = c.d_zero = nullptr;
 }
 
 int init_device_locked(int dev) {
@@ -353,6 +371,8 @@ int init_device_locked(int dev) {
     if ((e = hipMalloc(&c.d_unshift, img.unshift.size() * 4)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMalloc(&c.d_sb, img.sb.size() * 4)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMalloc(&c.d_stitch, img.stitch.size() * 4)) != hipSuccess) { rc = hip_fail(e); break; }
+    if ((e = hipMalloc(&c.d_stream_img, img.stream.size() * 4)) != hipSuccess) { rc = hip_fail(e); break; }
+    if ((e = hipMemcpy(c.d_stream_img, img.stream.data(), img.stream.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMalloc(&c.d_zero, 256)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMemset(c.d_zero, 0, 256)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMemcpy(c.d_sb, img.sb.data(), img.sb.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_fail(e); break; }
@@ -649,15 +669,7 @@ int run_arena(DeviceCtx& c, const void* d_base, size_t arena_bytes, const uint64
 // lengths, n) agree, are safe (sorted starts, gaps < 4 KiB) and dense (payload bytes >= 2/3 of the span).
 // The kernels then check this call's own extent against [lo, hi) on the device and, if it differs, read
 // nothing outside the payloads (each is folded directly) - a stale record costs time, never correctness
-// or a read of unmapped memory. Otherwise the sorted path runs. ANNETY_CRC_VAR_AUTO=0 keeps the sorted
-// path always.
-bool var_auto() {
-  static const bool on = [] {
-    const char* e = std::getenv("ANNETY_CRC_VAR_AUTO");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
+// or a read of unmapped memory. Otherwise the sorted path runs. (Mode 0 of run_var_any.)
 constexpr size_t kAutoMinPayloads = 1024;  // below this the extent kernel is not worth its launch
 // Arena calls between two that record their extent. In between, the arena launches skip the extent kernel
 // and the device check: the declared range is checked on the host to lie inside one device allocation
@@ -701,7 +713,7 @@ bool poll_hint(ScratchSlot* slot) {
 
 int run_var_auto(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_off, const uint32_t* d_len,
                  uint32_t* d_out, hipStream_t stream, bool update) {
-  if (!var_auto() || n < kAutoMinPayloads) return run_var_sorted(c, d_base, n, d_off, d_len, d_out, stream, update);
+  if (n < kAutoMinPayloads) return run_var_sorted(c, d_base, n, d_off, d_len, d_out, stream, update);
   std::lock_guard<std::mutex> lk(c.arena_mu);
   ScratchSlot* slot = nullptr;
   int rc = scratch_slot(c, stream, sorted_scratch_bytes(n), &slot);
@@ -767,6 +779,89 @@ int run_var_auto(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_o
   }
   const int rd = scratch_done(c, slot);
   return rc ? rc : rd;
+}
+
+// ---- line-stream path (crc32_stream.hip): any layout, no sort ----
+// Scratch inside the slot: desc (16 B per payload), posv (8 B), totals, pieces (16 B per stream wave).
+size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+size_t stream_scratch_bytes(size_t n, size_t waves) { return align256(16 * n) + align256(8 * n) + 256 + 16 * waves; }
+
+int run_var_stream(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_off, const uint32_t* d_len,
+                   uint32_t* d_out, hipStream_t stream, bool update) {
+  const size_t blocks = grid_cus(c), waves = blocks * (size_t)(fixed_kernel_block() / 64);
+  std::lock_guard<std::mutex> lk(c.arena_mu);
+  ScratchSlot* slot = nullptr;
+  int rc = scratch_slot(c, stream, stream_scratch_bytes(n, waves), &slot);
+  if (rc) return rc;
+  Scratch& d = slot->data;
+  const uint32_t ntiles = (uint32_t)((n + kStreamTile - 1) / kStreamTile);
+  const size_t set_words = kStreamSetHeader + (size_t)kStreamRecWords * ntiles;
+  if (d.st_set_words < set_words) {  // grown in stream order, like the slot's scratch
+    if (d.st) HIP_TRY(hipFreeAsync(d.st, stream));
+    d.st = nullptr;
+    d.st_set_words = 0;
+    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&d.st), 2 * set_words * sizeof(uint64_t), stream));
+    d.st_set_words = set_words;
+    d.st_clean = false;
+  }
+  if (!d.st_clean) {
+    HIP_TRY(hipMemsetAsync(d.st, 0, 2 * d.st_set_words * sizeof(uint64_t), stream));
+    d.st_clean = true;
+    d.st_used[0] = d.st_used[1] = 0;
+  }
+  const uint32_t set = (uint32_t)(d.st_calls & 1);
+  char* sc = path_scratch(slot);
+  StreamLaunch a{};
+  a.base = d_base;
+  a.off = d_off;
+  a.len = d_len;
+  a.n = n;
+  a.out = d_out;
+  a.update = update;
+  a.desc = sc;
+  a.posv = reinterpret_cast<uint64_t*>(sc + align256(16 * n));
+  a.totals = reinterpret_cast<uint64_t*>(sc + align256(16 * n) + align256(8 * n));
+  a.pieces = reinterpret_cast<uint4*>(sc + align256(16 * n) + align256(8 * n) + 256);
+  a.status = d.st + set * d.st_set_words;
+  a.status_other = d.st + (set ^ 1) * d.st_set_words;
+  a.other_words = d.st_used[set ^ 1] ? kStreamSetHeader + (size_t)kStreamRecWords * d.st_used[set ^ 1] : 0;
+  a.ntiles = ntiles;
+  a.img_slice = c.d_slice;
+  a.img_stream = c.d_stream_img;
+  a.zero_line = c.d_zero;
+  a.max_blocks = blocks;
+  const hipError_t e = launch_stream(a, stream);
+  if (e != hipSuccess) {
+    d.st_clean = false;  // a set may hold records: the next call zeroes both
+    rc = hip_fail(e);
+  } else {
+    d.st_used[set] = ntiles;
+    d.st_used[set ^ 1] = 0;
+    d.st_calls++;
+  }
+  const int rd = scratch_done(c, slot);
+  return rc ? rc : rd;
+}
+
+// The general variable path (annety_crc_set_var_path; initial value from ANNETY_CRC_VAR_PATH = auto / sorted /
+// stream, or ANNETY_CRC_VAR_AUTO=0 = sorted): 0 = automatic arena/sorted choice from recorded extents,
+// 1 = the length-sorted path, 2 = the line stream.
+std::atomic<int> g_var_mode{[] {
+  const char* e = std::getenv("ANNETY_CRC_VAR_PATH");
+  if (e && std::strcmp(e, "stream") == 0) return 2;
+  if (e && std::strcmp(e, "sorted") == 0) return 1;
+  if (e && std::strcmp(e, "auto") == 0) return 0;
+  const char* a = std::getenv("ANNETY_CRC_VAR_AUTO");
+  return a && a[0] == '0' ? 1 : 0;
+}()};
+
+int run_var_any(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_off, const uint32_t* d_len,
+                uint32_t* d_out, hipStream_t stream, bool update) {
+  switch (g_var_mode.load(std::memory_order_relaxed)) {
+    case 2: return run_var_stream(c, d_base, n, d_off, d_len, d_out, stream, update);
+    case 1: return run_var_sorted(c, d_base, n, d_off, d_len, d_out, stream, update);
+    default: return run_var_auto(c, d_base, n, d_off, d_len, d_out, stream, update);
+  }
 }
 
 bool fixed_fast_ok(const void* d_base, size_t len, size_t stride) {
@@ -921,6 +1016,7 @@ int annety_crc_shutdown(void) {
       HipSlotOps ops;
       c.slots.clear(ops, [](ScratchSlot& sl) {
         if (sl.data.ptr) (void)hipFree(sl.data.ptr);
+        if (sl.data.st) (void)hipFree(sl.data.st);
         if (sl.data.hint) (void)hipHostFree(sl.data.hint);
       });
     }
@@ -957,6 +1053,14 @@ int annety_crc_scratch_stats(int device, uint64_t* slots, uint64_t* handoffs, ui
   return ANNETY_CRC_OK;
 }
 
+int annety_crc_set_var_path(int mode) {
+  if (mode < 0 || mode > 2) return ANNETY_CRC_EINVAL;
+  g_var_mode.store(mode);
+  return ANNETY_CRC_OK;
+}
+
+int annety_crc_get_var_path(void) { return g_var_mode.load(); }
+
 int annety_crc_var_path_stats(int device, uint64_t* arena, uint64_t* sorted, uint64_t* arena_unrecorded) {
   if (device < 0 || device >= kMaxDev) return ANNETY_CRC_ENODEV;
   if (arena) *arena = g_dev[device].auto_arena.load();
@@ -975,6 +1079,7 @@ int annety_crc_stream_release(void* stream) {
   return c->slots.release(ops, s, s == hipStreamPerThread, [&](ScratchSlot& sl) -> int {
     // stream-ordered: the memory returns to the pool after the stream's queued work, nobody waits
     if (sl.data.ptr) HIP_TRY(hipFreeAsync(sl.data.ptr, s));
+    if (sl.data.st) HIP_TRY(hipFreeAsync(sl.data.st, s));
     if (sl.data.hint) {  // the stream's queued extent kernels may still write it: wait for them first
       HIP_TRY(hipStreamSynchronize(s));
       (void)hipHostFree(sl.data.hint);
@@ -1011,7 +1116,7 @@ int annety_crc32_batch_var(const void* d_base, const uint64_t* d_off, const uint
   int rc = stream_ctx(static_cast<hipStream_t>(stream), &c);
   if (rc) return rc;
   if (n > 0xFFFFFFFFull) return ANNETY_CRC_EINVAL;  // order[] holds 32-bit payload indices
-  return run_var_auto(*c, d_base, n, d_off, d_len, d_out, static_cast<hipStream_t>(stream), false);
+  return run_var_any(*c, d_base, n, d_off, d_len, d_out, static_cast<hipStream_t>(stream), false);
 }
 
 int annety_crc32_batch_var_arena(const void* d_arena, size_t arena_bytes, const uint64_t* d_off,
@@ -1058,7 +1163,7 @@ int annety_crc32_update_batch_var(uint32_t* d_state, const void* d_base, const u
   DeviceCtx* c = nullptr;
   int rc = stream_ctx(static_cast<hipStream_t>(stream), &c);
   if (rc) return rc;
-  return run_var_auto(*c, d_base, n, d_off, d_len, d_state, static_cast<hipStream_t>(stream), true);
+  return run_var_any(*c, d_base, n, d_off, d_len, d_state, static_cast<hipStream_t>(stream), true);
 }
 
 // Staging ring of the current device's context, allocated for at least `need` bytes per slot.

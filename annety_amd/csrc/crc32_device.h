@@ -148,6 +148,19 @@ __device__ __forceinline__ void absorb_two_lines(const uint4 (&v)[8], const uint
   rw = nibble_map_uniform(xc, lds, kLdsHalfOff) ^ xd;
 }
 
+// Map i of a set of T nibble-table maps stored [k][i][v] (k nibble position, v value): for one k the
+// set's tables lie side by side, so lanes applying different maps spread over the banks
+// ((16 i + v) mod 64) instead of all sharing the same 16 (a [i][k][v] layout cost the segment steps
+// up to 8-way conflicts).
+template <uint32_t T>
+__device__ __forceinline__ uint32_t nibble_map_set(uint32_t s, const uint32_t* lds, uint32_t off, uint32_t i) {
+  const uint32_t* t = lds + off / 4 + i * 16;
+  uint32_t r[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) r[k] = t[k * T * 16 + __builtin_amdgcn_ubfe(s, 4 * k, 4)];
+  return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6] ^ r[7]);
+}
+
 // Lane-position join: shift_{(G-1-j)*128}(s) from the replicated nibble tables (slot = lane & 31).
 __device__ __forceinline__ uint32_t nibble_map_lane(uint32_t s, const uint32_t* lds, uint32_t slot4) {
   const char* b = reinterpret_cast<const char*>(lds) + kLdsJoinOff;

@@ -187,6 +187,48 @@ inline ArenaGeom arena_geom(const ArenaLaunch& a) {
   return arena_geom(a, (size_t)want);
 }
 
+// Line-stream path (crc32_stream.hip): scan + stream + fixup launches, no host round trip. Scratch: desc
+// (16 B) and posv (8 B) per payload, totals (4 words), pieces (16 B per wave of the stream launch), and two
+// alternating status sets of the scan's look-back (kStreamSetHeader + kStreamRecWords words per tile).
+constexpr uint32_t kStreamTile = 2048;      // payloads per scan tile
+constexpr uint32_t kStreamSetHeader = 8;    // words: [0] the ticket counter
+constexpr uint32_t kStreamRecWords = 8;     // words per tile record
+struct StreamScanArgs {
+  const uint8_t* base;
+  const uint64_t* off;
+  const uint32_t* len;
+  size_t n;
+  uint32_t* out;          // empty payloads' digests (crc32_long mode)
+  uint4* desc;            // {addr lo, addr hi, len, index} of the k-th non-empty payload
+  uint64_t* posv;         // its first position (line of the stream)
+  uint64_t* totals;       // [0] non-empty payloads K, [1] positions, [2] nonzero = a look-back gave up
+  uint64_t* status;       // this call's set (zero on entry)
+  uint64_t* other;        // the previous call's set: zeroed here, other_words words
+  size_t other_words;
+  uint32_t ntiles;
+};
+struct StreamLaunch {
+  const void* base;
+  const uint64_t* off;
+  const uint32_t* len;
+  size_t n;
+  uint32_t* out;          // digests, or (update) registers in place
+  bool update;
+  void* desc;
+  uint64_t* posv;
+  uint64_t* totals;
+  uint4* pieces;          // 8 * max_blocks entries
+  uint64_t* status;
+  uint64_t* status_other;
+  size_t other_words;
+  uint32_t ntiles;        // ceil(n / kStreamTile)
+  const void* img_slice;  // common image part
+  const void* img_stream; // kStreamFixupBytes: stream part + power maps (crc32_math.h)
+  const void* zero_line;  // 128 zero bytes (device)
+  size_t max_blocks;      // stream launch grid (one workgroup per CU)
+};
+hipError_t launch_stream(const StreamLaunch& a, hipStream_t stream);
+
 hipError_t launch_arena(const ArenaLaunch& a, hipStream_t stream);
 // the line pass alone (crc32_arena.hip, crc32_arena_lines.h)
 hipError_t launch_arena_lines(const ArenaLaunch& a, hipStream_t stream);

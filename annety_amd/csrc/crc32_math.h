@@ -141,5 +141,19 @@ constexpr uint32_t kLdsStitchImageBytes = kLdsQuarterOff + 512;  // 160768 <= 16
 // layout (half-line join, segment maps, inverse shifts, quarter join) + shift_4 nibble map, 30 KiB.
 constexpr uint32_t kLdsWordOff = kLdsStitchImageBytes;  // in the stitch layout's coordinates
 constexpr uint32_t kLdsLiteBytes = kLdsWordOff + 512 - kLdsHalfOff;  // 30208
+// Line-stream variable path (crc32_stream.hip). Device image "stream" (offsets relative to its start):
+//   [0, 3 KiB)              scan maps S(i) = shift_{2^i * 128}, i = 0..5, each (k, v) at k*64 + v*4 (uniform)
+//   [3 KiB, +8 KiB)         U_lo set: shift_{-m}, m = 0..15, (k, m, v) at (k*16 + m)*64 + v*4
+//   [11 KiB, +4 KiB)        U_hi set: shift_{-16h}, h = 0..7, (k, h, v) at (k*8 + h)*64 + v*4
+//   [15 KiB, +16 KiB)       power maps P(i) = shift_{2^i * 128}, i = 0..31 (uniform; the cross-chunk fixup only)
+// The line-stream kernel stages [0, 15 KiB) behind the common part; the fixup stages all 31 KiB at 0.
+constexpr uint32_t kStreamScanOff = 0;
+constexpr uint32_t kStreamULoOff = 3072;
+constexpr uint32_t kStreamUHiOff = kStreamULoOff + 8192;
+constexpr uint32_t kStreamPartBytes = kStreamUHiOff + 4096;  // 15360
+constexpr uint32_t kStreamPowOff = kStreamPartBytes;
+constexpr uint32_t kStreamFixupBytes = kStreamPowOff + 32 * 512;  // 31744
+constexpr uint32_t kLdsStreamOff = kLdsCommonBytes;
+constexpr uint32_t kLdsStreamImageBytes = kLdsStreamOff + kStreamPartBytes;  // 146944
 
 }  // namespace annety_crc

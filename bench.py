@@ -63,10 +63,11 @@ def parse():
     p.add_argument("--strong", action="store_true",
                    help="fixed configs: --payloads (default 1M) is the TOTAL over all ranks, split into contiguous "
                         "shards (strong scaling); default is per GPU (weak scaling)")
-    p.add_argument("--var-path", choices=["arena", "auto", "sorted"], default="arena",
+    p.add_argument("--var-path", choices=["arena", "auto", "sorted", "stream"], default="arena",
                    help="config 3: arena = one pass over the packed arena + per-payload stitch (annety_crc32_batch_var_arena); "
                         "auto = annety_crc32_batch_var, which picks the arena path itself from the batch's recorded extent; "
-                        "sorted = the length-bucketed path only (ANNETY_CRC_VAR_AUTO=0)")
+                        "sorted = the length-bucketed path only (ANNETY_CRC_VAR_PATH=sorted); stream = the line-stream "
+                        "path (ANNETY_CRC_VAR_PATH=stream)")
     p.add_argument("--chunks", type=int, default=None,
                    help="N>1: chunks per shard for the pipelined gather (default 1 for config 1: step s's gather "
                         "overlaps step s+1's kernel; 2 for config 4, one-rank rehearsal 1/2/4 chunks "
@@ -220,7 +221,8 @@ class Workload:
             self.var_path = args.var_path
             self.desc = (f"BASELINE config 3: {self.n} payloads, Zipf(1.1) lengths 64 B-64 KiB packed unaligned, "
                          f"{total / 2**30:.3f} GiB per GPU, " + {"arena": "arena path", "auto": "automatic path choice",
-                                                                  "sorted": "sorted path"}[args.var_path])
+                                                                  "sorted": "sorted path",
+                                                                  "stream": "line-stream path"}[args.var_path])
         # strong scaling: shards differ by at most one payload; the digest buffer is padded (zeros) to the
         # largest so that every rank's gather moves the same count
         self.n_pad = -(-self.n_total // world) if getattr(args, "strong", False) else self.n
@@ -459,8 +461,8 @@ def main():
         raise SystemExit("--strong applies to the fixed 1 KiB configs (1, 4)")
     if args.chunks is None:
         args.chunks = 2 if args.config == 4 else 1
-    if args.var_path == "sorted":
-        os.environ["ANNETY_CRC_VAR_AUTO"] = "0"  # read once by the library: before it loads
+    if args.var_path in ("sorted", "stream", "auto"):
+        os.environ["ANNETY_CRC_VAR_PATH"] = args.var_path  # read once by the library: before it loads
     if multi and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < args.hw_queues:
         # HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default); the compute stream, torch's
         # RCCL stream and RCCL's own streams then share queues, and a queue runs its packets in order. Set
