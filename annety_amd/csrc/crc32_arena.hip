@@ -20,14 +20,15 @@
 //             E), appended to V(last line start).
 //     The whole lines between take at most four steps acc = M1(acc) ^ M2(S[a] ^ S[b]) (the head block,
 //     the partial superblocks' block runs, the tail block: M1 = shift by the unit, M2 = the inverse
-//     shift that cuts a suffix difference down to the unit) and one step per whole superblock between.
+//     shift that cuts a suffix difference down to the unit); the whole superblocks between join in one
+//     level, acc = shift_{n*8KiB}(acc) ^ xor_q shift_{(n-1-q)*8KiB}(SB[q, 0]), n independent lookups.
 //     A config-3 payload (6.5 KiB on average) costs 64 + 64 bytes of window folds and about six map
 //     steps of 8 nibble-table lookups, with every load issued before the first fold.
 //     s = 0xFFFFFFFF (crc32_long) or the caller's register (crc32_update, include/Crc32c.h:71-82).
 //     Bytes outside the arena [byte_lo, byte_hi) sharing a line with it are zeros to both launches.
 //
 // Reference semantics: crc32_long include/Crc32c.h:58-69 (digests), crc32_update :71-82 (update
-// mode); the math identities are in crc32_math.h. DESIGN.md §2.8.
+// mode); the math identities are in crc32_math.h. DESIGN.md §2.6.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -46,64 +47,30 @@ namespace {
 // returned wrong digests for whole waves now and then on the MI355X with the previous stitch - a
 // register-pressure-dependent fault we did not pin down)
 constexpr int kStitchBlock = 512;
+constexpr uint32_t kMidChunk = kMidMaps + 1;  // whole superblocks combined per level (P(1..7) and the identity)
 
 // (nibble_map_set: crc32_device.h)
-// ADJ: where the image starts in the full stitch layout (0, or kLdsHalfOff for the lite image, which
-// drops the slicing tables: see crc32_arena_stitch_lite_kernel).
 // shift_{-m} for m in [0, 128): U_hi[m >> 4] o U_lo[m & 15]
-template <uint32_t ADJ = 0>
 __device__ __forceinline__ uint32_t unshift(uint32_t t, uint32_t m, const uint32_t* lds) {
-  t = nibble_map_set<16>(t, lds, kLdsStitchUnshiftOff - ADJ, m & 15u);
-  return nibble_map_set<8>(t, lds, kLdsStitchUnshiftOff + 8192 - ADJ, m >> 4);
+  t = nibble_map_set<16>(t, lds, kLdsStitchUnshiftOff, m & 15u);
+  return nibble_map_set<8>(t, lds, kLdsStitchUnshiftOff + 8192, m >> 4);
 }
-template <uint32_t ADJ = 0>
 __device__ __forceinline__ uint32_t seg_map(uint32_t t, uint32_t idx, const uint32_t* lds) {
-  return nibble_map_set<32>(t, lds, kLdsMapOff - ADJ, idx);
+  return nibble_map_set<32>(t, lds, kLdsMapOff, idx);
+}
+// P(c) = shift_{c*8KiB} for a lane-varying c in 1..7: G(8) of the segment set for c = 1, else the mid set
+__device__ __forceinline__ uint32_t mid_map(uint32_t t, uint32_t c, const uint32_t* lds) {
+  const bool one = c == 1;
+  const uint32_t* b = lds + (one ? kLdsMapOff / 4 + (kMapG + 7) * 16 : kLdsMidOff / 4 + (c - 2) * 16);
+  const uint32_t stride = one ? 32 * 16 : kMidMaps * 16;
+  uint32_t r[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) r[k] = b[k * stride + __builtin_amdgcn_ubfe(t, 4 * k, 4)];
+  return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6] ^ r[7]);
 }
 
 __device__ __forceinline__ uint32_t gload4(uint64_t addr) {
   return *(const __attribute__((address_space(1))) uint32_t*)addr;
-}
-
-// Lite image (crc32_arena_stitch_lite_kernel): the window folds use a uniform nibble map shift_4 (8
-// conflict-free LDS reads per word) instead of the 128 KiB slicing tables. x = register ^ word becomes the
-// register after the word, pre-xored with the next one. Four 32-byte chains, as below.
-[[maybe_unused]] __device__ __forceinline__ void absorb_two_windows_lite(const uint4 (&v)[4], const uint4 (&w)[4], const uint32_t* lds,
-                                                        uint32_t off_word, uint32_t off_quarter, uint32_t& rv,
-                                                        uint32_t& rw) {
-  uint32_t xa = v[0].x, xb = v[2].x, xc = w[0].x, xd = w[2].x;
-#pragma unroll
-  for (int i = 0; i < 2; i++) {
-    const uint32_t na[4] = {v[i].y, v[i].z, v[i].w, i == 0 ? v[1].x : 0u};
-    const uint32_t nb[4] = {v[2 + i].y, v[2 + i].z, v[2 + i].w, i == 0 ? v[3].x : 0u};
-    const uint32_t nc[4] = {w[i].y, w[i].z, w[i].w, i == 0 ? w[1].x : 0u};
-    const uint32_t nd[4] = {w[2 + i].y, w[2 + i].z, w[2 + i].w, i == 0 ? w[3].x : 0u};
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      xa = nibble_map_uniform(xa, lds, off_word) ^ na[q];
-      xb = nibble_map_uniform(xb, lds, off_word) ^ nb[q];
-      xc = nibble_map_uniform(xc, lds, off_word) ^ nc[q];
-      xd = nibble_map_uniform(xd, lds, off_word) ^ nd[q];
-    }
-  }
-  rv = nibble_map_uniform(xa, lds, off_quarter) ^ xb;
-  rw = nibble_map_uniform(xc, lds, off_quarter) ^ xd;
-}
-// One 128-byte line from register 0 with the lite image: two 64-byte chains joined by shift_64.
-[[maybe_unused]] __device__ __forceinline__ uint32_t absorb_line_lite(const uint4 (&u)[8], const uint32_t* lds, uint32_t off_word,
-                                                     uint32_t off_half) {
-  uint32_t xa = u[0].x, xb = u[4].x;
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    const uint32_t na[4] = {u[i].y, u[i].z, u[i].w, i < 3 ? u[i + 1].x : 0u};
-    const uint32_t nb[4] = {u[4 + i].y, u[4 + i].z, u[4 + i].w, i < 3 ? u[5 + i].x : 0u};
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      xa = nibble_map_uniform(xa, lds, off_word) ^ na[q];
-      xb = nibble_map_uniform(xb, lds, off_word) ^ nb[q];
-    }
-  }
-  return nibble_map_uniform(xa, lds, off_half) ^ xb;
 }
 
 // Two 64-byte windows from register 0, four 32-byte chains: raw(window) = shift_32(raw(first half)) ^
@@ -142,6 +109,7 @@ struct StitchGeo {
   const uint64_t* check;  // ArenaLaunch::check
   uint32_t check_parts;
   uint64_t check_lo, check_hi;
+  bool check_any_order;
   ExtentHint* record;
   uint64_t record_seq;
 };
@@ -162,7 +130,7 @@ struct Plan {
 };
 struct Vals {
   uint4 h[4], t[4];
-  uint32_t x[4], y[4], mid[8];
+  uint32_t x[4], y[4], mid[kMidChunk];
   uint32_t s0;
 };
 
@@ -170,9 +138,10 @@ struct Vals {
 // B the S/SB words.
 //   PROBE (microbench only; product = 0): 1 = descriptors and stores only, 2 = + all loads,
 //   3 = + window folds (no map steps) - wrong digests, used to measure what the stages cost.
-template <bool UPD, int PROBE, bool LITE = false>
+//   MID (A/B): 1 = the whole superblocks between join in one level (mid_level), 0 = a chain of
+//   dependent shift_8KiB steps.
+template <bool UPD, int PROBE, bool MID = false>
 struct Stitcher {
-  static constexpr uint32_t ADJ = LITE ? kLdsHalfOff : 0u;
   const StitchGeo& g;
   const uint32_t* lds;
   LaneCtx k;
@@ -199,13 +168,26 @@ struct Stitcher {
     return edge ? ed : full;
   }
 
-  // SB[., 0] word indices of the whole superblocks mid_s .. mid_s + 7 (relative to sb0; the first n used, the
-  // rest 0). Whole superblocks between two partial ones are never the arena's edge superblocks, and SB is
-  // linear in the superblock, so no edge selects.
-  __device__ __forceinline__ void mid_addrs(uint32_t mid_s, uint32_t n, uint32_t (&a)[8]) const {
+  // SB[., 0] word indices of the whole superblocks mid_s .. mid_s + cnt - 1 (relative to sb0, cnt <= kMidChunk),
+  // the rest 0. MID: last first (a[c] is the superblock that ends c superblocks before the run's end, the term
+  // P(c) shifts); else in order. Whole superblocks between two partial ones are never the arena's edge superblocks, and SB
+  // is linear in the superblock, so no edge selects.
+  __device__ __forceinline__ void mid_addrs(uint32_t mid_s, uint32_t cnt, uint32_t (&a)[kMidChunk]) const {
     const uint32_t w0 = g.sb_word + (uint32_t)(g.sb0 + mid_s - g.fs0) * 8;
 #pragma unroll
-    for (uint32_t q = 0; q < 8; q++) a[q] = q < n ? w0 + 8 * q : 0u;
+    for (uint32_t c = 0; c < kMidChunk; c++) a[c] = c < cnt ? w0 + 8 * (MID ? cnt - 1 - c : c) : 0u;
+  }
+
+  // acc = P(cnt)(acc) ^ xor_c P(c)(w[c]) for cnt in 1..kMidChunk, P(c) = shift_{c*8KiB}: cnt whole superblocks
+  // (w[c] = SB[last - c, 0]) joined in one level of independent lookups instead of a chain of cnt dependent
+  // shift_8KiB steps
+  __device__ __forceinline__ uint32_t mid_level(uint32_t acc, uint32_t cnt, const uint32_t (&w)[kMidChunk]) const {
+    uint32_t t = mid_map(acc, cnt, lds) ^ w[0];
+    if (cnt > 1) t ^= seg_map(w[1], kMapG + 7, lds);
+#pragma unroll
+    for (uint32_t c = 2; c < kMidChunk; c++)
+      if (c < cnt) t ^= nibble_map_set<kMidMaps>(w[c], lds, kLdsMidOff, c - 2);
+    return t;
   }
 
   // Phase A: descriptor, plan, window and register loads (nothing the line pass writes).
@@ -290,10 +272,10 @@ struct Stitcher {
       v.x[q] = word(on ? y.xa[q] : dummy);
       v.y[q] = word(on && !((y.yzero >> q) & 1u) ? y.ya[q] : dummy);
     }
-    uint32_t ma[8];
-    mid_addrs(y.mid_s, y.nmid, ma);  // (dummy = 0)
+    uint32_t ma[kMidChunk];
+    mid_addrs(y.mid_s, y.nmid < kMidChunk ? y.nmid : kMidChunk, ma);  // (dummy = 0)
 #pragma unroll
-    for (int q = 0; q < 8; q++) v.mid[q] = word(ma[q]);
+    for (uint32_t c = 0; c < kMidChunk; c++) v.mid[c] = word(ma[c]);
   }
 
   __device__ __forceinline__ void process(size_t p, const Plan& y, Vals& v) const {
@@ -310,7 +292,7 @@ struct Stitcher {
 #pragma unroll
       for (int q = 0; q < 4; q++) t ^= v.h[q].x ^ v.t[q].y ^ v.x[q] ^ v.y[q];
 #pragma unroll
-      for (int q = 0; q < 8; q++) t ^= v.mid[q];
+      for (uint32_t c = 0; c < kMidChunk; c++) t ^= v.mid[c];
       g.out[p] = t;
       return;
     }
@@ -319,67 +301,75 @@ struct Stitcher {
       mask_line<4>(v.h, (int32_t)y.hlo * 8, (int32_t)y.hhi * 8);
       mask_line<4>(v.t, (int32_t)y.tlo * 8, (int32_t)y.thi * 8);
       uint32_t wh, wt;
-      if constexpr (LITE)
-        absorb_two_windows_lite(v.h, v.t, lds, kLdsWordOff - ADJ, kLdsQuarterOff - ADJ, wh, wt);
-      else
-        absorb_two_windows(v.h, v.t, k, lds, wh, wt);
+      absorb_two_windows(v.h, v.t, k, lds, wh, wt);
       // head: V(first line start) = shift_{-lead}(s0) ^ shift_{-64}(wh), or
       //       V(first line end) = shift_{-lead}(shift_128(s0)) ^ wh
-      const uint32_t f1s = seg_map<ADJ>(v.s0, kMapF, lds);
-      const uint32_t u64 = nibble_map_set<8>(wh, lds, kLdsStitchUnshiftOff + 8192 - ADJ, 4);  // shift_{-64}
-      acc = unshift<ADJ>(y.headX ? v.s0 : f1s, y.lead, lds) ^ (y.headX ? u64 : wh);
+      const uint32_t f1s = seg_map(v.s0, kMapF, lds);
+      const uint32_t u64 = nibble_map_set<8>(wh, lds, kLdsStitchUnshiftOff + 8192, 4);  // shift_{-64}
+      acc = unshift(y.headX ? v.s0 : f1s, y.lead, lds) ^ (y.headX ? u64 : wh);
       if constexpr (PROBE != 3) {
 #pragma unroll
         for (int q = 0; q < 2; q++) {
           if ((y.act >> q) & 1u) {
             const uint32_t d = v.x[q] ^ (((y.yzero >> q) & 1u) ? 0u : v.y[q]);
-            acc = seg_map<ADJ>(acc, __builtin_amdgcn_ubfe(y.m1, 8 * q, 5), lds) ^
-                  seg_map<ADJ>(d, __builtin_amdgcn_ubfe(y.m2, 8 * q, 5), lds);
+            acc = seg_map(acc, __builtin_amdgcn_ubfe(y.m1, 8 * q, 5), lds) ^
+                  seg_map(d, __builtin_amdgcn_ubfe(y.m2, 8 * q, 5), lds);
           }
         }
-        // whole superblocks between the partial ones: acc = shift_8KiB(acc) ^ SB[s,0]
-        for (uint32_t i = 0; i < y.nmid; i += 8) {
-          if (i > 0) {
-            uint32_t ma[8];
-            mid_addrs(y.mid_s + i, y.nmid - i, ma);
+        // whole superblocks between the partial ones, in one level per kMidChunk of them (the first chunk's
+        // words were loaded with the plan; payloads past 7 whole superblocks load the next chunks here)
+        if constexpr (MID) {
+          if (y.nmid) {
+            acc = mid_level(acc, y.nmid < kMidChunk ? y.nmid : kMidChunk, v.mid);
+            for (uint32_t i = kMidChunk; i < y.nmid; i += kMidChunk) {
+              const uint32_t cnt = y.nmid - i < kMidChunk ? y.nmid - i : kMidChunk;
+              uint32_t ma[kMidChunk], w[kMidChunk];
+              mid_addrs(y.mid_s + i, cnt, ma);
 #pragma unroll
-            for (int q = 0; q < 8; q++) v.mid[q] = word(ma[q]);
+              for (uint32_t c = 0; c < kMidChunk; c++) w[c] = word(ma[c]);
+              acc = mid_level(acc, cnt, w);
+            }
           }
+        } else {  // acc = shift_8KiB(acc) ^ SB[s, 0], superblock by superblock
+          for (uint32_t i = 0; i < y.nmid; i += kMidChunk) {
+            if (i > 0) {
+              uint32_t ma[kMidChunk];
+              mid_addrs(y.mid_s + i, y.nmid - i < kMidChunk ? y.nmid - i : kMidChunk, ma);
 #pragma unroll
-          for (int q = 0; q < 8; q++)
-            if (i + q < y.nmid) acc = seg_map<ADJ>(acc, kMapG + 7, lds) ^ v.mid[q];
+              for (uint32_t c = 0; c < kMidChunk; c++) v.mid[c] = word(ma[c]);
+            }
+#pragma unroll
+            for (uint32_t c = 0; c < kMidChunk; c++)
+              if (i + c < y.nmid) acc = seg_map(acc, kMapG + 7, lds) ^ v.mid[c];
+          }
         }
 #pragma unroll
         for (int q = 2; q < 4; q++) {
           if ((y.act >> q) & 1u) {
             const uint32_t d = v.x[q] ^ (((y.yzero >> q) & 1u) ? 0u : v.y[q]);
-            acc = seg_map<ADJ>(acc, __builtin_amdgcn_ubfe(y.m1, 8 * q, 5), lds) ^
-                  seg_map<ADJ>(d, __builtin_amdgcn_ubfe(y.m2, 8 * q, 5), lds);
+            acc = seg_map(acc, __builtin_amdgcn_ubfe(y.m1, 8 * q, 5), lds) ^
+                  seg_map(d, __builtin_amdgcn_ubfe(y.m2, 8 * q, 5), lds);
           }
         }
       }
       // tail: V(E) = shift_{-(128-te)}(V(last line end) ^ wt), or
       //       shift_{-(128-te)}(shift_128(V(last line start)) ^ shift_64(wt))
-      const uint32_t f1a = seg_map<ADJ>(acc, kMapF, lds);
-      const uint32_t h64 = nibble_map_uniform(wt, lds, kLdsHalfOff - ADJ);
-      acc = unshift<ADJ>(y.tailX ? acc ^ wt : f1a ^ h64, 128 - y.te, lds);
+      const uint32_t f1a = seg_map(acc, kMapF, lds);
+      const uint32_t h64 = nibble_map_uniform(wt, lds, kLdsHalfOff);
+      acc = unshift(y.tailX ? acc ^ wt : f1a ^ h64, 128 - y.te, lds);
     } else {
       // payload reaches outside the arena the caller declared (or there is none): fold its lines directly
       const uint64_t L0 = y.A >> 7, L1 = (y.E - 1) >> 7;
-      acc = unshift<ADJ>(v.s0, y.lead, lds);  // V(first line start): the lead bytes are zeros here
+      acc = unshift(v.s0, y.lead, lds);  // V(first line start): the lead bytes are zeros here
       for (uint64_t i = L0; i <= L1; i++) {
         uint4 u[8];
 #pragma unroll
         for (int q = 0; q < 8; q++) u[q] = gload16((i << 7) + 16 * q);
         mask_line<8>(u, i == L0 ? (int32_t)y.lead * 8 : 0, i == L1 ? (int32_t)y.te * 8 : 1024);
-        uint32_t r;
-        if constexpr (LITE)
-          r = absorb_line_lite(u, lds, kLdsWordOff - ADJ, kLdsHalfOff - ADJ);
-        else
-          r = absorb_line(0u, u, k, lds);
-        acc = seg_map<ADJ>(acc, kMapF, lds) ^ r;
+        const uint32_t r = absorb_line(0u, u, k, lds);
+        acc = seg_map(acc, kMapF, lds) ^ r;
       }
-      acc = unshift<ADJ>(acc, 128 - y.te, lds);  // drop the zero bytes after the payload end
+      acc = unshift(acc, 128 - y.te, lds);  // drop the zero bytes after the payload end
     }
     g.out[p] = UPD ? acc : ~acc;
   }
@@ -406,7 +396,7 @@ __device__ __forceinline__ void publish_extent(ExtentHint* host, uint64_t lo, ui
 // the same count for every block; the first payload's loads are in flight while the LDS image is staged.
 //   PIPE (microbench A/B, product = 0): 1 = the next payload's loads are issued before the
 //   current one is folded; 2 = a lane's first two payloads' descriptors and plan loads issued together.
-template <bool UPD, int BLK = kStitchBlock, int PROBE = 0, int PIPE = 0>
+template <bool UPD, int BLK = kStitchBlock, int PROBE = 0, int PIPE = 0, bool MID = false>
 __global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchGeo g0, const uint4* __restrict__ img_slice,
                                                                  const uint4* __restrict__ img_stitch) {
   __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsStitchImageBytes / 16];
@@ -416,11 +406,11 @@ __global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchGeo g0, c
   if (g.check) {
     uint64_t lo, hi, sum, bad;
     extent_of(g.check, g.check_parts, lo, hi, sum, bad);
-    if (!(lo == g.check_lo && hi == g.check_hi && bad == 0)) g.byte_lo = g.byte_hi = 0;
+    if (!(lo == g.check_lo && hi == g.check_hi && (bad == 0 || g.check_any_order))) g.byte_lo = g.byte_hi = 0;
     if (blockIdx.x == 0 && threadIdx.x == 0 && g.record)  // the next calls' record (crc32_kernels.h)
       publish_extent(g.record, lo, hi, sum, bad, g.record_seq);
   }
-  const Stitcher<UPD, PROBE> st{g, reinterpret_cast<const uint32_t*>(lds4), lane_ctx()};
+  const Stitcher<UPD, PROBE, MID> st{g, reinterpret_cast<const uint32_t*>(lds4), lane_ctx()};
   const size_t per = (g.n + gridDim.x - 1) / gridDim.x;
   const size_t p_end = std::min(g.n, (size_t)(blockIdx.x + 1) * per);
   const size_t p_first = (size_t)blockIdx.x * per + threadIdx.x;
@@ -486,33 +476,6 @@ __global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchGeo g0, c
       }
       st.process(p, y, v);
     }
-  }
-}
-
-// Lite stitch (microbench A/B): the image without the slicing tables (30 KiB instead of 157 KiB), so
-// several blocks fit a CU; one payload per lane, WPE = minimum waves per SIMD the compiler must allow.
-template <bool UPD, int BLK, int WPE>
-__global__ __launch_bounds__(BLK) __attribute__((amdgpu_waves_per_eu(WPE))) void crc32_arena_stitch_lite_kernel(
-    StitchGeo g, const uint4* __restrict__ img_lite) {
-  __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsLiteBytes / 16];
-  const Stitcher<UPD, 0, true> st{g, reinterpret_cast<const uint32_t*>(lds4), lane_ctx()};
-  const size_t per = (g.n + gridDim.x - 1) / gridDim.x;
-  const size_t p_end = std::min(g.n, (size_t)(blockIdx.x + 1) * per);
-  const size_t p_first = (size_t)blockIdx.x * per + threadIdx.x;
-  Plan y{};
-  Vals v{};
-  if (p_first < p_end) {
-    st.plan_a(p_first, y, v);
-    st.plan_b(p_first, y, v);
-  }
-  load_image<kLdsLiteBytes, BLK>(lds4, img_lite, nullptr);
-  __syncthreads();
-  for (size_t p = p_first; p < p_end; p += BLK) {
-    if (p != p_first) {
-      st.plan_a(p, y, v);
-      st.plan_b(p, y, v);
-    }
-    st.process(p, y, v);
   }
 }
 
@@ -727,6 +690,7 @@ LineOut line_out(const ArenaLaunch& a, const ArenaGeom& geo) {
   ar.check = a.check;
   ar.check_parts = a.check_parts;
   ar.check_lo = a.check_lo;
+  ar.check_any_order = a.check_any_order;
   ar.check_hi = a.check_hi;
   return ar;
 }
@@ -763,13 +727,14 @@ StitchGeo stitch_geo(const ArenaLaunch& a, const ArenaGeom& geo) {
   s.check = a.check;
   s.check_parts = a.check_parts;
   s.check_lo = a.check_lo;
+  s.check_any_order = a.check_any_order;
   s.check_hi = a.check_hi;
   s.record = a.record;
   s.record_seq = a.record_seq;
   return s;
 }
 
-template <int PROBE, int PIPE = 0, int BLK = kStitchBlock>
+template <int PROBE, int PIPE = 0, int BLK = kStitchBlock, bool MID = false>
 hipError_t launch_stitch_p(const ArenaLaunch& a, hipStream_t stream) {
   const StitchGeo s = stitch_geo(a, arena_geom(a));
   const size_t blocks = stitch_blocks(a, BLK);
@@ -777,24 +742,11 @@ hipError_t launch_stitch_p(const ArenaLaunch& a, hipStream_t stream) {
   const uint4* img_stitch = static_cast<const uint4*>(a.img_stitch);
   note_kernel("crc32_arena_stitch_kernel");
   if (a.update)
-    hipLaunchKernelGGL((crc32_arena_stitch_kernel<true, BLK, PROBE, PIPE>), dim3((unsigned)blocks), dim3(BLK), 0,
+    hipLaunchKernelGGL((crc32_arena_stitch_kernel<true, BLK, PROBE, PIPE, MID>), dim3((unsigned)blocks), dim3(BLK), 0,
                        stream, s, img_slice, img_stitch);
   else
-    hipLaunchKernelGGL((crc32_arena_stitch_kernel<false, BLK, PROBE, PIPE>), dim3((unsigned)blocks), dim3(BLK), 0,
+    hipLaunchKernelGGL((crc32_arena_stitch_kernel<false, BLK, PROBE, PIPE, MID>), dim3((unsigned)blocks), dim3(BLK), 0,
                        stream, s, img_slice, img_stitch);
-  return hipGetLastError();
-}
-
-// blocks: 0 = one payload per lane (ceil(n / BLK))
-template <int BLK, int WPE>
-hipError_t launch_stitch_lite(const ArenaLaunch& a, const void* img_lite, size_t blocks, hipStream_t stream) {
-  const StitchGeo s = stitch_geo(a, arena_geom(a));
-  if (!blocks) blocks = std::max<size_t>(1, (a.n + BLK - 1) / BLK);
-  const uint4* img = static_cast<const uint4*>(img_lite);
-  if (a.update)
-    hipLaunchKernelGGL((crc32_arena_stitch_lite_kernel<true, BLK, WPE>), dim3((unsigned)blocks), dim3(BLK), 0, stream, s, img);
-  else
-    hipLaunchKernelGGL((crc32_arena_stitch_lite_kernel<false, BLK, WPE>), dim3((unsigned)blocks), dim3(BLK), 0, stream, s, img);
   return hipGetLastError();
 }
 
@@ -833,6 +785,12 @@ hipError_t launch_arena(const ArenaLaunch& a, hipStream_t stream) {
     const char* e = std::getenv("ANNETY_CRC_STITCH_PIPE");
     return !(e && e[0] == '0');
   }();
+  // ANNETY_CRC_STITCH_MID=1: the one-level superblock join (mid_level), which fits the VGPRs only without PIPE
+  static const bool mid = [] {
+    const char* e = std::getenv("ANNETY_CRC_STITCH_MID");
+    return e && e[0] == '1';
+  }();
+  if (mid) return launch_stitch_p<0, 0, kStitchBlock, true>(a, stream);
   return pipe ? launch_stitch_p<0, 1>(a, stream) : launch_stitch_p<0>(a, stream);
 }
 

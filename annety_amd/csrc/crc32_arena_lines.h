@@ -18,6 +18,7 @@ struct LineOut {
   const uint64_t* check;  // ArenaLaunch::check
   uint32_t check_parts;
   uint64_t check_lo, check_hi;
+  bool check_any_order;
 };
 
 // This call's extent from the launch_extent partials (ws + 8 + 4b: {lo, hi, sum, bad} of block b), reduced
@@ -41,12 +42,14 @@ __device__ __forceinline__ void extent_of(const uint64_t* ws, uint32_t parts, ui
     bad |= (uint64_t)__shfl_xor((unsigned long long)bad, d);
   }
 }
-// ArenaLaunch::check: this call's extent equals the declared one and the batch is safe.
-__device__ __forceinline__ bool extent_matches(const uint64_t* check, uint32_t parts, uint64_t lo, uint64_t hi) {
+// ArenaLaunch::check: this call's extent equals the declared one and the batch is safe (sorted with small gaps,
+// or any order when the host found the declared span inside one allocation: any_order).
+__device__ __forceinline__ bool extent_matches(const uint64_t* check, uint32_t parts, uint64_t lo, uint64_t hi,
+                                               bool any_order) {
   if (!check) return true;
   uint64_t l, h, s, b;
   extent_of(check, parts, l, h, s, b);
-  return l == lo && h == hi && b == 0;
+  return l == lo && h == hi && (b == 0 || any_order);
 }
 
 //   PROBE (microbench only; product = 0): bit 0 drops the S stores, bit 1 the superblock scan, bit 2 only
@@ -72,7 +75,7 @@ __device__ __forceinline__ void arena_line_pass(const uint8_t* __restrict__ base
                                                 const uint4* __restrict__ img_sb) {
   constexpr int BLK = kBlock, VWG = kVwg;
   // uniform over the grid: on a mismatch the stitch folds every payload directly
-  if (!extent_matches(ar.check, ar.check_parts, ar.check_lo, ar.check_hi)) return;
+  if (!extent_matches(ar.check, ar.check_parts, ar.check_lo, ar.check_hi, ar.check_any_order)) return;
   const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
   const uint32_t j = threadIdx.x & 7;
   const size_t gid = (((size_t)bid + (size_t)nbid * (threadIdx.x / VWG)) * VWG + threadIdx.x % VWG) / 8;

@@ -207,14 +207,21 @@ const HostImages& host_images() {
       put_set(m + (kLdsStitchUnshiftOff - kLdsMapOff) / 4, img.unshift.data(), 16);                  // U_lo
       put_set(m + (kLdsStitchUnshiftOff + 8192 - kLdsMapOff) / 4, img.unshift.data() + 16 * 128, 8);  // U_hi
       nibble_tables(shift_matrix(32), m + (kLdsQuarterOff - kLdsMapOff) / 4);
+      std::vector<uint32_t> mid(kMidMaps * 128);  // P(c) = shift_{c*8KiB}, c = 2..7
+      for (uint32_t c = 2; c < 2 + kMidMaps; c++) nibble_tables(shift_matrix((uint64_t)8192 * c), mid.data() + (c - 2) * 128);
+      put_set(m + (kLdsMidOff - kLdsMapOff) / 4, mid.data(), kMidMaps);
     }
-    img.stream.assign(kStreamFixupBytes / 4, 0);
+    img.stream.assign(kStreamImgBytes / 4, 0);
     {
       uint32_t* m = img.stream.data();
-      for (uint32_t i = 0; i < 6; i++) nibble_tables(shift_matrix((uint64_t)kChunkBytes << i), m + (kStreamScanOff + 512 * i) / 4);
       put_set(m + kStreamULoOff / 4, img.unshift.data(), 16);
       put_set(m + kStreamUHiOff / 4, img.unshift.data() + 16 * 128, 8);
-      for (uint32_t i = 0; i < 32; i++) nibble_tables(shift_matrix((uint64_t)kChunkBytes << i), m + (kStreamPowOff + 512 * i) / 4);
+      for (uint32_t a = 0; a < 128; a++) m[kStreamInitOff / 4 + a] = shift_bits(kInit, 8u * (128 - a));
+      for (uint32_t i = 0; i < 6; i++) nibble_tables(shift_matrix((uint64_t)kChunkBytes << i), m + (kStreamPowOff + 512 * i) / 4);
+      for (uint32_t i = 0; i < 32; i++) {
+        const Gf2Mat g = shift_matrix((uint64_t)kChunkBytes << i);
+        std::memcpy(m + kStreamMatOff / 4 + 32 * i, g.col, sizeof g.col);
+      }
     }
   });
   return img;
@@ -666,7 +673,8 @@ int run_arena(DeviceCtx& c, const void* d_base, size_t arena_bytes, const uint64
 // back would make every call synchronous. Instead every call launches the extent kernel (crc32_kernels.h
 // launch_extent, ~5 us), which leaves the batch's extent in a pinned record per stream slot, and a call
 // takes the arena path over [lo, hi) when the two latest completed records for the same (base, offsets,
-// lengths, n) agree, are safe (sorted starts, gaps < 4 KiB) and dense (payload bytes >= 2/3 of the span).
+// lengths, n) agree, are dense (payload bytes >= 2/3 of the span) and safe (sorted starts with gaps < 4 KiB, or
+// in any order when the span lies inside one device allocation).
 // The kernels then check this call's own extent against [lo, hi) on the device and, if it differs, read
 // nothing outside the payloads (each is folded directly) - a stale record costs time, never correctness
 // or a read of unmapped memory. Otherwise the sorted path runs. (Mode 0 of run_var_any.)
@@ -731,12 +739,17 @@ int run_var_auto(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_o
   }
   poll_hint(slot);
   const ExtentHint& h = slot->data.seen;
-  const bool arena = slot->data.seen_seq >= slot->data.key_since && slot->data.prev_seq >= slot->data.key_since && !h.bad &&
-                     h.hi > h.lo && h.lo == slot->data.prev.lo && h.hi == slot->data.prev.hi && !slot->data.prev.bad &&
-                     h.sum * 3 >= (h.hi - h.lo) * 2 && h.hi - h.lo < (32ull << 30);
+  const uint64_t b = (uint64_t)(uintptr_t)d_base;
+  bool arena = slot->data.seen_seq >= slot->data.key_since && slot->data.prev_seq >= slot->data.key_since &&
+               h.hi > h.lo && h.lo == slot->data.prev.lo && h.hi == slot->data.prev.hi &&
+               h.sum * 3 >= (h.hi - h.lo) * 2 && h.hi - h.lo < (32ull << 30);
+  // Safe: sorted starts with gaps < 4 KiB put every byte of the span on a page holding payload bytes; any
+  // other order or gap qualifies when the span lies inside one device allocation (the arena's cost follows
+  // the span, which the density bound above keeps within 1.5x the payload bytes, in any order).
+  const bool any_order = arena && (h.bad || slot->data.prev.bad);
+  if (any_order) arena = range_mapped(b + h.lo, b + h.hi);
   ArenaLaunch a{};
   if (arena) {
-    const uint64_t b = (uint64_t)(uintptr_t)d_base;
     arena_fill_range(c, d_base, b + h.lo, b + h.hi, a);
     a.off = d_off;
     a.len = d_len;
@@ -745,6 +758,7 @@ int run_var_auto(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_o
     a.update = update;
     a.check_lo = h.lo;
     a.check_hi = h.hi;
+    a.check_any_order = any_order;
     if (a.nsb && (rc = scratch_slot(c, stream, arena_geom(a).words * sizeof(uint32_t), &slot))) return rc;
     if (++slot->data.since_extent < kAutoRefresh && range_mapped(b + h.lo, b + h.hi)) {
       // between two recording calls: the arena launches alone (kAutoRefresh above)
@@ -782,9 +796,12 @@ int run_var_auto(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_o
 }
 
 // ---- line-stream path (crc32_stream.hip): any layout, no sort ----
-// Scratch inside the slot: desc (16 B per payload), posv (8 B), totals, pieces (16 B per stream wave).
+// Scratch inside the slot: desc (16 B per payload), posv (8 B), edges (8 B), totals, pieces (16 B per stream wave)
+// and join counters (4 B per stream wave).
 size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
-size_t stream_scratch_bytes(size_t n, size_t waves) { return align256(16 * n) + align256(8 * n) + 256 + 16 * waves; }
+size_t stream_scratch_bytes(size_t n, size_t waves) {
+  return align256(16 * n) + 2 * align256(8 * n) + 256 + 16 * waves + 4 * waves;
+}
 
 int run_var_stream(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_off, const uint32_t* d_len,
                    uint32_t* d_out, hipStream_t stream, bool update) {
@@ -820,8 +837,10 @@ int run_var_stream(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d
   a.update = update;
   a.desc = sc;
   a.posv = reinterpret_cast<uint64_t*>(sc + align256(16 * n));
-  a.totals = reinterpret_cast<uint64_t*>(sc + align256(16 * n) + align256(8 * n));
-  a.pieces = reinterpret_cast<uint4*>(sc + align256(16 * n) + align256(8 * n) + 256);
+  a.edges = reinterpret_cast<uint32_t*>(sc + align256(16 * n) + align256(8 * n));
+  a.totals = reinterpret_cast<uint64_t*>(sc + align256(16 * n) + 2 * align256(8 * n));
+  a.pieces = reinterpret_cast<uint4*>(sc + align256(16 * n) + 2 * align256(8 * n) + 256);
+  a.counters = reinterpret_cast<uint32_t*>(sc + align256(16 * n) + 2 * align256(8 * n) + 256 + 16 * waves);
   a.status = d.st + set * d.st_set_words;
   a.status_other = d.st + (set ^ 1) * d.st_set_words;
   a.other_words = d.st_used[set ^ 1] ? kStreamSetHeader + (size_t)kStreamRecWords * d.st_used[set ^ 1] : 0;

@@ -103,6 +103,7 @@ struct ArenaLaunch {
   const uint64_t* check;
   uint32_t check_parts;
   uint64_t check_lo, check_hi;
+  bool check_any_order;      // the recorded span lies in one allocation: unsorted or gapped batches qualify
   ExtentHint* record;
   uint64_t record_seq;
 };
@@ -187,8 +188,9 @@ inline ArenaGeom arena_geom(const ArenaLaunch& a) {
   return arena_geom(a, (size_t)want);
 }
 
-// Line-stream path (crc32_stream.hip): scan + stream + fixup launches, no host round trip. Scratch: desc
-// (16 B) and posv (8 B) per payload, totals (4 words), pieces (16 B per wave of the stream launch), and two
+// Line-stream path (crc32_stream.hip): scan + stream launches, no host round trip. Scratch: desc (16 B), posv
+// (8 B) and edges (8 B) per payload, totals (4 words), pieces (16 B) and a join counter (4 B) per wave of the
+// stream launch, and two
 // alternating status sets of the scan's look-back (kStreamSetHeader + kStreamRecWords words per tile).
 constexpr uint32_t kStreamTile = 2048;      // payloads per scan tile
 constexpr uint32_t kStreamSetHeader = 8;    // words: [0] the ticket counter
@@ -206,6 +208,21 @@ struct StreamScanArgs {
   uint64_t* other;        // the previous call's set: zeroed here, other_words words
   size_t other_words;
   uint32_t ntiles;
+  uint32_t* counters;     // the stream launch's join counters (one per wave), zeroed here
+  size_t ncounters;
+};
+struct StreamArgs {       // the stream launch (crc32_stream.hip)
+  const uint4* desc;
+  const uint64_t* posv;
+  const uint64_t* totals;
+  uint32_t* edges;
+  uint32_t* out;
+  uint4* pieces;
+  uint32_t* counters;
+  const uint8_t* zero_line;
+  const uint4* img_slice;
+  const uint4* img_stream;
+  const uint32_t* mats;   // the power matrices (img_stream + kStreamMatOff)
 };
 struct StreamLaunch {
   const void* base;
@@ -217,13 +234,15 @@ struct StreamLaunch {
   void* desc;
   uint64_t* posv;
   uint64_t* totals;
+  uint32_t* edges;        // 2 words per non-empty payload: its first and last line's masked CRC
   uint4* pieces;          // 8 * max_blocks entries
+  uint32_t* counters;     // 8 * max_blocks entries
   uint64_t* status;
   uint64_t* status_other;
   size_t other_words;
   uint32_t ntiles;        // ceil(n / kStreamTile)
   const void* img_slice;  // common image part
-  const void* img_stream; // kStreamFixupBytes: stream part + power maps (crc32_math.h)
+  const void* img_stream; // kStreamImgBytes (crc32_math.h): the LDS part, then the power matrices
   const void* zero_line;  // 128 zero bytes (device)
   size_t max_blocks;      // stream launch grid (one workgroup per CU)
 };

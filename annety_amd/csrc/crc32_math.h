@@ -131,29 +131,33 @@ constexpr uint32_t kLdsArenaNtImageBytes = kLdsArenaImageBytes + kLdsByteMapByte
 //   [kLdsStitchUnshiftOff, +8 KiB)  set U_lo[m] = shift_{-m}, (k, m, v) at (k*16 + m)*64 + v*4
 //   [+8 KiB, +12 KiB)                set U_hi[h] = shift_{-16h}, (k, h, v) at (k*8 + h)*64 + v*4
 //   [kLdsQuarterOff, +512)  shift_32 (joins the two 32-byte chains of a half-line window)
+//   [kLdsMidOff, +3 KiB)    set P(m) = shift_{m*8KiB}, m = 2..7, (k, m-2, v) at (k*6 + m-2)*64 + v*4: the whole
+//                           superblocks between a payload's partial ones, combined in one level
 constexpr uint32_t kLdsMapOff = kLdsCommonBytes;
 constexpr uint32_t kLdsMapBytes = 32 * 512;
 constexpr uint32_t kMapF = 0, kMapG = 8, kMapUL = 16, kMapUB = 24;  // map index of F(1), G(1), UL(0), UB(0)
 constexpr uint32_t kLdsStitchUnshiftOff = kLdsMapOff + kLdsMapBytes;
 constexpr uint32_t kLdsQuarterOff = kLdsStitchUnshiftOff + kLdsUnshiftBytes;
-constexpr uint32_t kLdsStitchImageBytes = kLdsQuarterOff + 512;  // 160768 <= 163840
-// Lite stitch image (crc32_arena_stitch_lite_kernel): [kLdsHalfOff, kLdsStitchImageBytes) of the stitch
-// layout (half-line join, segment maps, inverse shifts, quarter join) + shift_4 nibble map, 30 KiB.
-constexpr uint32_t kLdsWordOff = kLdsStitchImageBytes;  // in the stitch layout's coordinates
-constexpr uint32_t kLdsLiteBytes = kLdsWordOff + 512 - kLdsHalfOff;  // 30208
-// Line-stream variable path (crc32_stream.hip). Device image "stream" (offsets relative to its start):
-//   [0, 3 KiB)              scan maps S(i) = shift_{2^i * 128}, i = 0..5, each (k, v) at k*64 + v*4 (uniform)
-//   [3 KiB, +8 KiB)         U_lo set: shift_{-m}, m = 0..15, (k, m, v) at (k*16 + m)*64 + v*4
-//   [11 KiB, +4 KiB)        U_hi set: shift_{-16h}, h = 0..7, (k, h, v) at (k*8 + h)*64 + v*4
-//   [15 KiB, +16 KiB)       power maps P(i) = shift_{2^i * 128}, i = 0..31 (uniform; the cross-chunk fixup only)
-// The line-stream kernel stages [0, 15 KiB) behind the common part; the fixup stages all 31 KiB at 0.
-constexpr uint32_t kStreamScanOff = 0;
-constexpr uint32_t kStreamULoOff = 3072;
-constexpr uint32_t kStreamUHiOff = kStreamULoOff + 8192;
-constexpr uint32_t kStreamPartBytes = kStreamUHiOff + 4096;  // 15360
-constexpr uint32_t kStreamPowOff = kStreamPartBytes;
-constexpr uint32_t kStreamFixupBytes = kStreamPowOff + 32 * 512;  // 31744
+constexpr uint32_t kLdsMidOff = kLdsQuarterOff + 512;
+constexpr uint32_t kMidMaps = 6;  // P(2..7); P(1) = G(8) of the segment set, P(0) = identity
+constexpr uint32_t kLdsStitchImageBytes = kLdsMidOff + kMidMaps * 512;  // 163840: all of the CU's LDS
+// Line-stream variable path (crc32_stream.hip). Device image "stream" (offsets relative to its start); the
+// line-stream kernel stages [0, kStreamPartBytes) behind the common part:
+//   [0, 8 KiB)              U_lo set: shift_{-m}, m = 0..15, (k, m, v) at (k*16 + m)*64 + v*4
+//   [8 KiB, +4 KiB)         U_hi set: shift_{-16h}, h = 0..7, (k, h, v) at (k*8 + h)*64 + v*4
+//   [12 KiB, +512 B)        init terms I[a] = shift_{128-a}(0xFFFFFFFF), a = 0..127: crc32_long's init seen from
+//                           the end of the line whose byte a starts the payload
+//   [12.5 KiB, +3 KiB)      scan maps P(i) = shift_{2^i * 128}, i = 0..5, each (k, v) at k*64 + v*4 (uniform)
+//   [15.5 KiB, +4 KiB)      (global only) power matrices M(i) = shift_{2^i * 128}, i = 0..31, 32 columns each:
+//                           the cross-chunk join, read with scalar loads
+constexpr uint32_t kStreamULoOff = 0;
+constexpr uint32_t kStreamUHiOff = 8192;
+constexpr uint32_t kStreamInitOff = 12288;
+constexpr uint32_t kStreamPowOff = 12800;
+constexpr uint32_t kStreamPartBytes = kStreamPowOff + 6 * 512;  // 15872
+constexpr uint32_t kStreamMatOff = kStreamPartBytes;
+constexpr uint32_t kStreamImgBytes = kStreamMatOff + 32 * 32 * 4;  // 19968
 constexpr uint32_t kLdsStreamOff = kLdsCommonBytes;
-constexpr uint32_t kLdsStreamImageBytes = kLdsStreamOff + kStreamPartBytes;  // 146944
+constexpr uint32_t kLdsStreamImageBytes = kLdsStreamOff + kStreamPartBytes;  // 147456
 
 }  // namespace annety_crc

@@ -174,3 +174,32 @@ def test_unrecorded_arena_calls_between_records(gpu):
         _check(out, data, cur, lens)
     s1 = annety_amd.var_path_stats(0)
     assert s1["arena_unrecorded"] - s0["arena_unrecorded"] >= 10, (s0, s1)
+
+
+@pytest.mark.parametrize("layout", ["shuffled", "gapped"])
+def test_dense_unsorted_or_gapped_batch_moves_to_arena(gpu, layout):
+    """Dense batches (payload bytes >= 2/3 of the span) in any order, or with gaps of 4 KiB and more, take the
+    arena path once the span is seen to lie inside one device allocation (crc32_capi.cpp run_var_auto,
+    check_any_order); the device check then accepts the recorded extent whatever its order."""
+    import torch
+
+    import annety_amd
+
+    if layout == "shuffled":
+        data, offs, lens = _packed(7, 5000)
+        perm = np.random.default_rng(8).permutation(len(offs))
+        offs, lens = offs[perm].copy(), lens[perm].copy()
+    else:
+        rng = np.random.default_rng(9)
+        lens = rng.integers(40000, 65536, 600).astype(np.int64)
+        offs = np.concatenate([[0], np.cumsum(lens + 5000)[:-1]]).astype(np.int64)  # 5 KiB gaps, ~90% dense
+        data = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 256, dtype=np.uint8)
+    d, o, ln = _dev(gpu, data, offs, lens)
+    out = torch.empty(len(lens), dtype=torch.int32, device=gpu)
+    s0 = annety_amd.var_path_stats(0)
+    for _ in range(12):
+        out.fill_(7)
+        annety_amd.crc32_batch_var(d, o, ln, out=out)
+        _check(out, data, offs, lens)
+    s1 = annety_amd.var_path_stats(0)
+    assert s1["sorted"] - s0["sorted"] == 2 and s1["arena"] - s0["arena"] == 10, (s0, s1)
