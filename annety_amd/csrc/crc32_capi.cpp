@@ -592,7 +592,7 @@ int run_var_sorted_in(DeviceCtx& c, ScratchSlot* slot, const void* d_base, size_
     a.img_unshift = c.d_unshift;
     a.out = d_out;
     a.max_blocks = grid_cus(c);
-    const hipError_t e = launch_var_sorted(a, group_image(c, 32), group_image(c, 16), group_image(c, 4), stream);
+    const hipError_t e = launch_var_sorted(a, group_image(c, 32), group_image(c, 16), group_image(c, 4), group_image(c, 8), stream);
     return e == hipSuccess ? ANNETY_CRC_OK : hip_fail(e);
   }
   const uint32_t groups[3] = {32, 16, 4};  // lanes per payload of the long / middle / small class

@@ -51,7 +51,7 @@ hipError_t launch_var(const VarLaunch& a, hipStream_t stream);
 // The sorted path's three length classes (G = 32 / 16 / 4, a.range = their 6 bounds) in one launch;
 // a.group and a.img_group are ignored.
 hipError_t launch_var_sorted(const VarLaunch& a, const void* img_g32, const void* img_g16, const void* img_g4,
-                             hipStream_t stream);
+                             const void* img_g8, hipStream_t stream);
 
 // Long payloads cut into end-aligned segments (crc32_kernels.hip): descriptors for the variable kernel,
 // then the combine fold with powers[(m-1)*32 + bit] = shift_{m*seg}(1 << bit), m = 1..S-1.

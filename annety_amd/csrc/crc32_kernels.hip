@@ -602,6 +602,358 @@ __device__ __forceinline__ void var_class(uint4* lds4, const uint8_t* __restrict
   }
 }
 
+// Byte masks of one half-line (bytes [64 h, 64 h + 64) of a payload line, h = the lane's l3), for the line with
+// real index li (var_class's masks, per half): li < 0 = virtual (zero), li = 0 the first line (bytes before the
+// payload dropped, the init or the caller's register on payload bytes 0..3), li = 1 the spill line when the
+// first holds fewer than 4 payload bytes, li = nlines - 1 the last (bytes after the payload dropped).
+//   keep bits [A8, H8) of the line; non-UPD: complement bits [A8, B8) (the init); UPD: xor the register at S8.
+struct HalfMask {
+  int32_t A8, B8, H8, S8;
+  uint32_t reg;
+  uint32_t need;  // some byte of the line changes
+};
+template <bool UPD>
+__device__ __forceinline__ HalfMask half_mask(int32_t li, const VarTask& cur) {
+  HalfMask m;
+  const bool first = li == 0;
+  const bool spill = li == 1 && cur.lead > 124 && cur.len >= 4;
+  m.A8 = li < 0 ? 1024 : (first ? (int32_t)cur.lead * 8 : 0);
+  m.H8 = li == (int32_t)cur.nlines - 1 ? (int32_t)cur.tailend * 8 : 1024;
+  m.S8 = first || spill ? ((int32_t)cur.lead - (first ? 0 : 128)) * 8 : 4096;  // register byte 0 (UPD)
+  m.reg = cur.len < 4 ? 0u : cur.state;
+  m.B8 = first || spill ? (cur.len < 4 ? m.A8 : ((int32_t)cur.lead + 4 - (first ? 0 : 128)) * 8) : m.A8;
+  m.need = (li < 2 || li >= (int32_t)cur.nlines - 1) ? 1u : 0u;
+  return m;
+}
+template <bool UPD, int O>
+__device__ __forceinline__ void apply_half_mask(uint4 (&v)[8], const HalfMask& m, uint32_t h) {
+  const int32_t base8 = (int32_t)h * 512;  // bit offset of the half in its line
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    uint32_t* w = reinterpret_cast<uint32_t*>(&v[O + i]);
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int32_t p8 = base8 + (i * 16 + q * 4) * 8;
+      const uint32_t keepA = (uint32_t)(0xFFFFFFFFull << clamp032(m.A8 - p8));
+      const uint32_t keepH = (uint32_t)(0xFFFFFFFFull >> clamp032(p8 + 32 - m.H8));
+      if constexpr (UPD) {
+        const int32_t x = m.S8 - p8;
+        const uint32_t sw = x >= 32 || x <= -32 ? 0u : (x >= 0 ? m.reg << x : m.reg >> -x);
+        w[q] = (keepA & keepH & w[q]) ^ sw;
+      } else {
+        const uint32_t keepB = (uint32_t)(0xFFFFFFFFull << clamp032(m.B8 - p8));
+        w[q] = keepA & keepH & (w[q] ^ ~keepB);
+      }
+    }
+  }
+}
+template <bool UPD, int O>
+__device__ __forceinline__ void mask_half(uint4 (&v)[8], int32_t li, const VarTask& cur, uint32_t h) {
+  apply_half_mask<UPD, O>(v, half_mask<UPD>(li, cur), h);
+}
+__device__ __forceinline__ int32_t lane_xor8(int32_t x) { return __builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, false); }
+
+// The G = 32 and G = 16 length classes with coalesced nontemporal loads (crc32_fixed32_nt_kernel's access
+// shape on the sorted descriptors). A wave holds NG = 64 / G lane groups, each stepping through its own
+// (payload, round) sequence exactly like var_class<G>; per step a group's round is G consecutive absolute lines,
+// read as 1 KiB pieces: load i covers piece 2 (i >> 2) + (i & 1) of group (i >> 1) & 1 (G = 32) or piece i >> 2
+// of group i & 3 (G = 16), with the groups' line bases broadcast from their first lanes. A lane's line index is
+// clamped to its payload's lines (virtual lines of the first round re-read the first line and are masked to
+// zero; a group without a task reads one line of the buffer). After transpose_blocks lane l holds half l3 of
+// lines jA and jA + G/2 of its group's round (jA = 8 l4 + (l & 7) for G = 32, l & 7 for G = 16); both halves
+// are masked where they hold a payload edge, the round register enters the first halves, and the half join
+// leaves lane l the register of line jl = jA + (G/2) l3 (nibble-table half join: the var image has no byte
+// tables). STAGE as var_class (1: the whole image, also for a block without work; 0: the group part only).
+template <int G, bool UPD, int STAGE>
+__device__ __forceinline__ void var_class_nt(uint4* lds4, const uint8_t* __restrict__ base,
+                                             const uint4* __restrict__ desc, const uint32_t* __restrict__ range,
+                                             const uint4* __restrict__ img_slice, const uint4* __restrict__ img_group,
+                                             const uint4* __restrict__ img_unshift, uint32_t* __restrict__ out) {
+  static_assert(G == 16 || G == 32, "two or four lane groups per wave");
+  constexpr int NG = 64 / G;
+  const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
+  const uint32_t l = threadIdx.x & 63, l3 = (l >> 3) & 1, l4 = (l >> 4) & 1;
+  const size_t gid = group_id<kBlock, G, kVwg>();
+  const size_t ngroups = ((size_t)gridDim.x * kBlock) / G;
+  const size_t t_begin = range[0], t_end = range[1];
+  LaneCtx k;
+  k.L0 = (threadIdx.x & 31) << 3;
+  k.L1 = k.L0 | (1u << 16);
+  const uint32_t jA = (G == 32 ? 8 * l4 : 0u) + (l & 7);  // line of v[0..3]; v[4..7] holds line jA + G/2
+  const uint32_t jl = jA + (G / 2) * l3;
+  k.slot4 = jl << 2;
+  const uint32_t chunk = 16u * (4u * l3 + 2u * ((l >> 5) & 1u) + l4);  // coalesced_lane_offset without the line
+  const uint64_t b0 = (uint64_t)(uintptr_t)base;
+  const uint64_t safe_line = b0 >> 7;
+
+  auto raw = [&](size_t t) { return raw_task<true>(t, t_end, base, desc, 0, 0); };
+  auto load = [&](const VarTask& tk, uint32_t r, uint4 (&v)[8]) {
+    const int32_t rel0 = (int32_t)(r * G) - (int32_t)tk.vlead;
+    const int32_t rmax = tk.valid ? (int32_t)tk.nlines - 1 : 0;
+    const uint64_t ln0 = tk.valid ? tk.line0 : safe_line;
+    const uint32_t lo = (uint32_t)ln0, hi = (uint32_t)(ln0 >> 32);
+    int32_t rel_g[NG], max_g[NG];
+    uint64_t ln_g[NG];
+#pragma unroll
+    for (int g = 0; g < NG; g++) {
+      rel_g[g] = __builtin_amdgcn_readlane(rel0, g * G);
+      max_g[g] = __builtin_amdgcn_readlane(rmax, g * G);
+      ln_g[g] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, g * G) << 32) |
+                (uint32_t)__builtin_amdgcn_readlane((int)lo, g * G);
+    }
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int g = G == 32 ? (i >> 1) & 1 : i & 3;
+      const int piece = G == 32 ? 2 * (i >> 2) + (i & 1) : i >> 2;
+      const int32_t rel = min(max(rel_g[g] + 8 * piece + (int32_t)(l & 7), 0), max_g[g]);
+      const uint64_t off = ((ln_g[g] + (uint64_t)rel) << 7) + chunk - b0;
+      const v4u32 x = __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(base + off));
+      v[i] = make_uint4(x.x, x.y, x.z, x.w);
+    }
+  };
+
+  size_t t0 = t_begin + gid;
+  if (!__syncthreads_or(t0 < t_end)) {  // the block has no task of this class
+    if constexpr (STAGE == 1) {  // (the next classes stage only their group part)
+      load_image<kLdsVarImageBytes>(lds4, img_slice, img_group, img_unshift);
+      __syncthreads();
+    }
+    return;
+  }
+  VarTask dec0 = decode_task<G>(raw(t0), t0 < t_end);
+  if constexpr (UPD) dec0.state = dec0.valid ? out[dec0.p] : 0u;
+  uint32_t r0 = 0;
+  size_t t1 = dec0.rounds > 1 ? t0 : t0 + ngroups;
+  uint32_t r1 = dec0.rounds > 1 ? 1u : 0u;
+  uint4 d1 = raw(t1);
+
+  uint4 A[8], B[8];
+  load(dec0, r0, A);
+  if constexpr (STAGE == 0)
+    load_image<kLdsImageBytes, kBlock, kLdsImageBytes, kLdsCommonBytes>(lds4, img_slice, img_group);
+  else
+    load_image<kLdsVarImageBytes>(lds4, img_slice, img_group, img_unshift);
+  __syncthreads();
+
+  uint32_t s = 0;
+  auto compute = [&](uint4 (&v)[8], const VarTask& cur, uint32_t r_c) {
+    transpose_blocks(v);
+    const int32_t liA = (int32_t)(r_c * G + jA) - (int32_t)cur.vlead;
+    const int32_t liB = liA + G / 2;
+    const int32_t last = (int32_t)cur.nlines - 1;
+    if (liA < 2 || liA >= last) mask_half<UPD, 0>(v, liA, cur, l3);
+    if (liB < 2 || liB >= last) mask_half<UPD, 4>(v, liB, cur, l3);
+    // the round register (shift_{(G-1)*128} of the lane's register, 0 at a payload's first round) enters the
+    // first half of its line: lanes with l3 = 0 fold the first halves of their own line and of lane ^ 8's
+    const uint32_t sin = nibble_map_uniform(s, lds, kLdsRoundOff);
+    const uint32_t sp = (uint32_t)__builtin_amdgcn_mov_dpp((int)sin, 0x128, 0xF, 0xF, false);  // lane ^ 8's
+    v[0].x ^= l3 ? 0u : sin;
+    v[4].x ^= l3 ? 0u : sp;
+    {
+      uint32_t xa = v[0].x, xb = v[4].x;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        word4x2(xa, v[i].y, xb, v[4 + i].y, k);
+        word4x2(xa, v[i].z, xb, v[4 + i].z, k);
+        word4x2(xa, v[i].w, xb, v[4 + i].w, k);
+        word4x2(xa, i + 1 < 4 ? v[i + 1].x : 0u, xb, i + 1 < 4 ? v[5 + i].x : 0u, k);
+      }
+      const uint32_t send = l3 ? xa : xb;
+      const uint32_t got = (uint32_t)__builtin_amdgcn_mov_dpp((int)send, 0x128, 0xF, 0xF, false);
+      const uint32_t first = l3 ? got : xa, second = l3 ? xb : got;
+      s = nibble_map_uniform(first, lds, kLdsHalfOff) ^ second;  // shift_64
+    }
+    if (r_c == cur.rounds - 1) {
+      uint32_t t = group_xor_reduce<G>(nibble_map_lane(s, lds, k.slot4));
+      if (cur.valid && (l & (G - 1)) == G - 1) {
+        const uint32_t over = 128 - cur.tailend;  // trailing zero bytes of the last line
+        if (over) {
+          t = nibble_map_uniform(t, lds, kLdsUnshiftOff + (over & 15u) * 512);
+          t = nibble_map_uniform(t, lds, kLdsUnshiftOff + 8192 + (over >> 4) * 512);
+        }
+        if constexpr (UPD) {
+          if (cur.len < 4) t ^= shift_bits(cur.state, 8u * cur.len);
+          out[cur.p] = t;
+        } else {
+          if (cur.len < 4) {
+            constexpr uint32_t k1 = shift_bits(kInit, 8), k2 = shift_bits(kInit, 16), k3 = shift_bits(kInit, 24);
+            t ^= cur.len == 1 ? k1 : (cur.len == 2 ? k2 : k3);
+          }
+          out[cur.p] = ~t;
+        }
+      }
+      s = 0;
+    }
+  };
+
+  auto step = [&](uint4 (&cur_buf)[8], uint4 (&nxt_buf)[8]) {
+    VarTask dec1 = decode_task<G>(d1, t1 < t_end);
+    if constexpr (UPD) dec1.state = dec1.valid ? out[dec1.p] : 0u;
+    const bool more = r1 + 1 < dec1.rounds;
+    const size_t t2 = more ? t1 : t1 + ngroups;
+    const uint32_t r2 = more ? r1 + 1 : 0u;
+    const uint4 d2 = raw(t2);
+    ANNETY_PRIO_HI();
+    load(dec1, r1, nxt_buf);
+    __builtin_amdgcn_sched_barrier(0);
+    ANNETY_PRIO_LO();
+    compute(cur_buf, dec0, r0);
+    dec0 = dec1;
+    r0 = r1;
+    t1 = t2;
+    r1 = r2;
+    d1 = d2;
+  };
+
+  // wave-uniform loop: the loads and the cross-lane steps need every group (a finished group reads one
+  // line of the buffer and stores nothing)
+  while (__builtin_amdgcn_ballot_w64(dec0.valid) != 0) {
+    step(A, B);
+    step(B, A);
+  }
+}
+
+// The small class (< 24 lines) with coalesced nontemporal loads, at G = 8: a wave's eight lane groups (lanes
+// 8m..8m+7) each step through their own (payload, round) sequence, a round being 8 consecutive absolute lines =
+// 1 KiB = exactly one load. Load i reads the round of lane group m(i) = (i >> 2) + 2 (i & 1) + 4 ((i >> 1) & 1)
+// (its line base broadcast from lane 8 m(i)), so that after transpose_blocks and the half join lane l holds
+// line l & 7 of its own group's round (crc32_onekib_nt_kernel's layout). Before the join a lane holds half l3 of
+// line l & 7 of two groups: its own and lane ^ 8's; the masks of the partner's line come over DPP.
+template <bool UPD>
+__device__ __forceinline__ void var_class_nt8(uint4* lds4, const uint8_t* __restrict__ base,
+                                              const uint4* __restrict__ desc, const uint32_t* __restrict__ range,
+                                              const uint4* __restrict__ img_slice, const uint4* __restrict__ img_group,
+                                              uint32_t* __restrict__ out) {
+  constexpr int G = 8;
+  const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
+  const uint32_t l = threadIdx.x & 63, l3 = (l >> 3) & 1, j = l & 7;
+  const size_t gid = group_id<kBlock, G, kVwg>();
+  const size_t ngroups = ((size_t)gridDim.x * kBlock) / G;
+  const size_t t_begin = range[0], t_end = range[1];
+  LaneCtx k;
+  k.L0 = (threadIdx.x & 31) << 3;
+  k.L1 = k.L0 | (1u << 16);
+  k.slot4 = (threadIdx.x & 31) << 2;  // join slot: j = slot & 7
+  const uint32_t lane_off = coalesced_lane_offset(l);
+  const uint64_t b0 = (uint64_t)(uintptr_t)base;
+  const uint64_t safe_line = b0 >> 7;
+
+  auto raw = [&](size_t t) { return raw_task<true>(t, t_end, base, desc, 0, 0); };
+  auto load = [&](const VarTask& tk, uint32_t r, uint4 (&v)[8]) {
+    const int32_t rel0 = (int32_t)(r * G) - (int32_t)tk.vlead;
+    const int32_t rmax = tk.valid ? (int32_t)tk.nlines - 1 : 0;
+    const uint64_t ln0 = tk.valid ? tk.line0 : safe_line;
+    const uint32_t lo = (uint32_t)ln0, hi = (uint32_t)(ln0 >> 32);
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int src = 8 * ((i >> 2) + 2 * (i & 1) + 4 * ((i >> 1) & 1));
+      const int32_t rel_g = __builtin_amdgcn_readlane(rel0, src), max_g = __builtin_amdgcn_readlane(rmax, src);
+      const uint64_t ln_g = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, src) << 32) |
+                            (uint32_t)__builtin_amdgcn_readlane((int)lo, src);
+      const int32_t rel = min(max(rel_g + (int32_t)j, 0), max_g);
+      const uint64_t off = ((ln_g + (uint64_t)rel) << 7) + (lane_off & 127u) - b0;
+      const v4u32 x = __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(base + off));
+      v[i] = make_uint4(x.x, x.y, x.z, x.w);
+    }
+  };
+
+  size_t t0 = t_begin + gid;
+  if (!__syncthreads_or(t0 < t_end)) return;
+  VarTask dec0 = decode_task<G>(raw(t0), t0 < t_end);
+  if constexpr (UPD) dec0.state = dec0.valid ? out[dec0.p] : 0u;
+  uint32_t r0 = 0;
+  size_t t1 = dec0.rounds > 1 ? t0 : t0 + ngroups;
+  uint32_t r1 = dec0.rounds > 1 ? 1u : 0u;
+  uint4 d1 = raw(t1);
+
+  uint4 A[8], B[8];
+  load(dec0, r0, A);
+  load_image<kLdsImageBytes, kBlock, kLdsImageBytes, kLdsCommonBytes>(lds4, img_slice, img_group);
+  __syncthreads();
+
+  uint32_t s = 0;
+  auto compute = [&](uint4 (&v)[8], const VarTask& cur, uint32_t r_c) {
+    transpose_blocks(v);
+    const int32_t li = (int32_t)(r_c * G + j) - (int32_t)cur.vlead;
+    const HalfMask mo = half_mask<UPD>(li, cur);
+    HalfMask mp;  // lane ^ 8's line (same position j in the partner group)
+    mp.A8 = lane_xor8(mo.A8);
+    mp.H8 = lane_xor8(mo.H8);
+    if constexpr (UPD) {
+      mp.S8 = lane_xor8(mo.S8);
+      mp.reg = (uint32_t)lane_xor8((int32_t)mo.reg);
+    } else {
+      mp.B8 = lane_xor8(mo.B8);
+    }
+    mp.need = (uint32_t)lane_xor8((int32_t)mo.need);
+    // v[0..3]: half l3 of the line of lane l & ~8's group, v[4..7]: of lane l | 8's
+    if (l3 ? mp.need : mo.need) apply_half_mask<UPD, 0>(v, l3 ? mp : mo, l3);
+    if (l3 ? mo.need : mp.need) apply_half_mask<UPD, 4>(v, l3 ? mo : mp, l3);
+    const uint32_t sin = nibble_map_uniform(s, lds, kLdsRoundOff);  // shift_{7*128}; 0 at a first round
+    const uint32_t sp = (uint32_t)lane_xor8((int32_t)sin);
+    v[0].x ^= l3 ? 0u : sin;
+    v[4].x ^= l3 ? 0u : sp;
+    {
+      uint32_t xa = v[0].x, xb = v[4].x;
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        word4x2(xa, v[i].y, xb, v[4 + i].y, k);
+        word4x2(xa, v[i].z, xb, v[4 + i].z, k);
+        word4x2(xa, v[i].w, xb, v[4 + i].w, k);
+        word4x2(xa, i + 1 < 4 ? v[i + 1].x : 0u, xb, i + 1 < 4 ? v[5 + i].x : 0u, k);
+      }
+      const uint32_t send = l3 ? xa : xb;
+      const uint32_t got = (uint32_t)lane_xor8((int32_t)send);
+      const uint32_t first = l3 ? got : xa, second = l3 ? xb : got;
+      s = nibble_map_uniform(first, lds, kLdsHalfOff) ^ second;  // shift_64
+    }
+    if (r_c == cur.rounds - 1) {
+      uint32_t t = group_xor_reduce<G>(nibble_map_lane(s, lds, k.slot4));
+      if (cur.valid && j == G - 1) {
+        const uint32_t over = 128 - cur.tailend;
+        if (over) {
+          t = nibble_map_uniform(t, lds, kLdsUnshiftOff + (over & 15u) * 512);
+          t = nibble_map_uniform(t, lds, kLdsUnshiftOff + 8192 + (over >> 4) * 512);
+        }
+        if constexpr (UPD) {
+          if (cur.len < 4) t ^= shift_bits(cur.state, 8u * cur.len);
+          out[cur.p] = t;
+        } else {
+          if (cur.len < 4) {
+            constexpr uint32_t k1 = shift_bits(kInit, 8), k2 = shift_bits(kInit, 16), k3 = shift_bits(kInit, 24);
+            t ^= cur.len == 1 ? k1 : (cur.len == 2 ? k2 : k3);
+          }
+          out[cur.p] = ~t;
+        }
+      }
+      s = 0;
+    }
+  };
+
+  auto step = [&](uint4 (&cur_buf)[8], uint4 (&nxt_buf)[8]) {
+    VarTask dec1 = decode_task<G>(d1, t1 < t_end);
+    if constexpr (UPD) dec1.state = dec1.valid ? out[dec1.p] : 0u;
+    const bool more = r1 + 1 < dec1.rounds;
+    const size_t t2 = more ? t1 : t1 + ngroups;
+    const uint32_t r2 = more ? r1 + 1 : 0u;
+    const uint4 d2 = raw(t2);
+    ANNETY_PRIO_HI();
+    load(dec1, r1, nxt_buf);
+    __builtin_amdgcn_sched_barrier(0);
+    ANNETY_PRIO_LO();
+    compute(cur_buf, dec0, r0);
+    dec0 = dec1;
+    r0 = r1;
+    t1 = t2;
+    r1 = r2;
+    d1 = d2;
+  };
+  while (__builtin_amdgcn_ballot_w64(dec0.valid) != 0) {
+    step(A, B);
+    step(B, A);
+  }
+}
+
 template <int G, bool SORTED, bool UPD = false, int VWG = kVwg, int PROBE = 0>
 __global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __restrict__ base, size_t n,
                                                            uint64_t fstride, uint32_t flen,
@@ -621,7 +973,9 @@ __global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __rest
 // the group part of the image), then of the G = 4 class. A block that finishes a class early starts the
 // next one instead of waiting for the class's slowest lane groups (three launches drained each class:
 // a 64 KiB-payload launch loses ~24 us to its tail), and two launch gaps go.
-template <bool UPD>
+//   NT: every class with coalesced nontemporal loads (var_class_nt at G = 32 / 16, var_class_nt8 for the small
+//   class at G = 8); ANNETY_CRC_SORTED_NT=0 = per-line loads (the small class at G = 4).
+template <bool UPD, bool NT>
 __global__ __launch_bounds__(kBlock) void crc32_var_sorted_kernel(const uint8_t* __restrict__ base, size_t n,
                                                                   const uint4* __restrict__ desc,
                                                                   const uint32_t* __restrict__ ranges,
@@ -629,14 +983,24 @@ __global__ __launch_bounds__(kBlock) void crc32_var_sorted_kernel(const uint8_t*
                                                                   const uint4* __restrict__ img_g32,
                                                                   const uint4* __restrict__ img_g16,
                                                                   const uint4* __restrict__ img_g4,
+                                                                  const uint4* __restrict__ img_g8,
                                                                   const uint4* __restrict__ img_unshift,
                                                                   uint32_t* __restrict__ out) {
   __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsVarImageBytes / 16];
-  var_class<32, true, UPD, kVwg, 0, 1>(lds4, base, n, 0, 0, desc, ranges, img_slice, img_g32, img_unshift, out);
+  if constexpr (NT)
+    var_class_nt<32, UPD, 1>(lds4, base, desc, ranges, img_slice, img_g32, img_unshift, out);
+  else
+    var_class<32, true, UPD, kVwg, 0, 1>(lds4, base, n, 0, 0, desc, ranges, img_slice, img_g32, img_unshift, out);
   __syncthreads();  // every wave is done with the G = 32 group tables
-  var_class<16, true, UPD, kVwg, 0, 0>(lds4, base, n, 0, 0, desc, ranges + 2, img_slice, img_g16, img_unshift, out);
+  if constexpr (NT)
+    var_class_nt<16, UPD, 0>(lds4, base, desc, ranges + 2, img_slice, img_g16, img_unshift, out);
+  else
+    var_class<16, true, UPD, kVwg, 0, 0>(lds4, base, n, 0, 0, desc, ranges + 2, img_slice, img_g16, img_unshift, out);
   __syncthreads();
-  var_class<4, true, UPD, kVwg, 0, 0>(lds4, base, n, 0, 0, desc, ranges + 4, img_slice, img_g4, img_unshift, out);
+  if constexpr (NT)
+    var_class_nt8<UPD>(lds4, base, desc, ranges + 4, img_slice, img_g8, out);
+  else
+    var_class<4, true, UPD, kVwg, 0, 0>(lds4, base, n, 0, 0, desc, ranges + 4, img_slice, img_g4, img_unshift, out);
 }
 
 // ---- long payloads: segments + CRC combine ----
@@ -823,17 +1187,27 @@ hipError_t launch_fixed(const FixedLaunch& a, hipStream_t stream) {
 }
 
 hipError_t launch_var_sorted(const VarLaunch& a, const void* img_g32, const void* img_g16, const void* img_g4,
-                             hipStream_t stream) {
+                             const void* img_g8, hipStream_t stream) {
   const unsigned blocks = (unsigned)std::max<size_t>(1, a.max_blocks);
   note_kernel("crc32_var_sorted_kernel");
-#define ANNETY_SORTED_LAUNCH(UPD)                                                                             \
-  hipLaunchKernelGGL((crc32_var_sorted_kernel<UPD>), dim3(blocks), dim3(kBlock), 0, stream,                  \
+#define ANNETY_SORTED_LAUNCH(UPD, NT)                                                                         \
+  hipLaunchKernelGGL((crc32_var_sorted_kernel<UPD, NT>), dim3(blocks), dim3(kBlock), 0, stream,              \
                      static_cast<const uint8_t*>(a.base), a.n, static_cast<const uint4*>(a.desc), a.range,      \
                      static_cast<const uint4*>(a.img_slice), static_cast<const uint4*>(img_g32),               \
                      static_cast<const uint4*>(img_g16), static_cast<const uint4*>(img_g4),                    \
+                     static_cast<const uint4*>(img_g8),                                                         \
                      static_cast<const uint4*>(a.img_unshift), a.out)
-  if (a.update) ANNETY_SORTED_LAUNCH(true);
-  else ANNETY_SORTED_LAUNCH(false);
+  static const bool nt = [] {
+    const char* e = std::getenv("ANNETY_CRC_SORTED_NT");
+    return !(e && e[0] == '0');
+  }();
+  if (a.update) {
+    if (nt) ANNETY_SORTED_LAUNCH(true, true);
+    else ANNETY_SORTED_LAUNCH(true, false);
+  } else {
+    if (nt) ANNETY_SORTED_LAUNCH(false, true);
+    else ANNETY_SORTED_LAUNCH(false, false);
+  }
 #undef ANNETY_SORTED_LAUNCH
   return hipGetLastError();
 }

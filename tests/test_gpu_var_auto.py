@@ -63,7 +63,7 @@ def test_sparse_batch_stays_sorted(gpu):
 
     import annety_amd
 
-    data, offs, lens = _packed(2, 3000, gap=5000)  # gaps >= 4 KiB: never the arena path
+    data, offs, lens = _packed(2, 3000, gap=40000)  # payload bytes ~20 % of the span: never the arena path
     d, o, ln = _dev(gpu, data, offs, lens)
     out = torch.empty(len(lens), dtype=torch.int32, device=gpu)
     s0 = annety_amd.var_path_stats(0)
@@ -191,7 +191,7 @@ def test_dense_unsorted_or_gapped_batch_moves_to_arena(gpu, layout):
         offs, lens = offs[perm].copy(), lens[perm].copy()
     else:
         rng = np.random.default_rng(9)
-        lens = rng.integers(40000, 65536, 600).astype(np.int64)
+        lens = rng.integers(40000, 65536, 1100).astype(np.int64)
         offs = np.concatenate([[0], np.cumsum(lens + 5000)[:-1]]).astype(np.int64)  # 5 KiB gaps, ~90% dense
         data = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 256, dtype=np.uint8)
     d, o, ln = _dev(gpu, data, offs, lens)
