@@ -973,9 +973,12 @@ __global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __rest
 // the group part of the image), then of the G = 4 class. A block that finishes a class early starts the
 // next one instead of waiting for the class's slowest lane groups (three launches drained each class:
 // a 64 KiB-payload launch loses ~24 us to its tail), and two launch gaps go.
-//   NT: every class with coalesced nontemporal loads (var_class_nt at G = 32 / 16, var_class_nt8 for the small
-//   class at G = 8); ANNETY_CRC_SORTED_NT=0 = per-line loads (the small class at G = 4).
-template <bool UPD, bool NT>
+//   NT (bits, ANNETY_CRC_SORTED_NT, default 3): 1 = the G = 32 class with coalesced nontemporal loads
+//   (var_class_nt), 2 = the G = 16 class too, 4 = the small class at G = 8 (var_class_nt8); unset classes load
+//   per line (small: G = 4). Config 3, one class alone (profiles/r04/sorted_nt/classes.log): G = 32 150.4 us
+//   coalesced / 182.6 per line, G = 16 68.6 / 63.8, small 53.2 (G = 8) / 40.9 (G = 4); fused, masks 1 and 3 the
+//   same, 7 slower.
+template <bool UPD, int NT>
 __global__ __launch_bounds__(kBlock) void crc32_var_sorted_kernel(const uint8_t* __restrict__ base, size_t n,
                                                                   const uint4* __restrict__ desc,
                                                                   const uint32_t* __restrict__ ranges,
@@ -985,19 +988,28 @@ __global__ __launch_bounds__(kBlock) void crc32_var_sorted_kernel(const uint8_t*
                                                                   const uint4* __restrict__ img_g4,
                                                                   const uint4* __restrict__ img_g8,
                                                                   const uint4* __restrict__ img_unshift,
-                                                                  uint32_t* __restrict__ out) {
+                                                                  uint32_t* __restrict__ out, uint32_t classes) {
   __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsVarImageBytes / 16];
-  if constexpr (NT)
-    var_class_nt<32, UPD, 1>(lds4, base, desc, ranges, img_slice, img_g32, img_unshift, out);
-  else
-    var_class<32, true, UPD, kVwg, 0, 1>(lds4, base, n, 0, 0, desc, ranges, img_slice, img_g32, img_unshift, out);
+  // classes: bit c runs class c (7 in the product; the microbench timing of one class alone leaves digests
+  // of the others unwritten, ANNETY_CRC_SORTED_CLASSES)
+  if (classes & 1) {
+    if constexpr (NT & 1)
+      var_class_nt<32, UPD, 1>(lds4, base, desc, ranges, img_slice, img_g32, img_unshift, out);
+    else
+      var_class<32, true, UPD, kVwg, 0, 1>(lds4, base, n, 0, 0, desc, ranges, img_slice, img_g32, img_unshift, out);
+  } else {
+    load_image<kLdsVarImageBytes>(lds4, img_slice, img_g32, img_unshift);
+  }
   __syncthreads();  // every wave is done with the G = 32 group tables
-  if constexpr (NT)
-    var_class_nt<16, UPD, 0>(lds4, base, desc, ranges + 2, img_slice, img_g16, img_unshift, out);
-  else
-    var_class<16, true, UPD, kVwg, 0, 0>(lds4, base, n, 0, 0, desc, ranges + 2, img_slice, img_g16, img_unshift, out);
+  if (classes & 2) {
+    if constexpr (NT & 2)
+      var_class_nt<16, UPD, 0>(lds4, base, desc, ranges + 2, img_slice, img_g16, img_unshift, out);
+    else
+      var_class<16, true, UPD, kVwg, 0, 0>(lds4, base, n, 0, 0, desc, ranges + 2, img_slice, img_g16, img_unshift, out);
+  }
   __syncthreads();
-  if constexpr (NT)
+  if (!(classes & 4)) return;
+  if constexpr (NT & 4)
     var_class_nt8<UPD>(lds4, base, desc, ranges + 4, img_slice, img_g8, out);
   else
     var_class<4, true, UPD, kVwg, 0, 0>(lds4, base, n, 0, 0, desc, ranges + 4, img_slice, img_g4, img_unshift, out);
@@ -1186,6 +1198,8 @@ hipError_t launch_fixed(const FixedLaunch& a, hipStream_t stream) {
   return a.full ? launch_full<true, false>(a, stream) : launch_full<false, false>(a, stream);
 }
 
+constexpr int kSortedNtDefault = 3;  // crc32_var_sorted_kernel NT: G = 32 and G = 16 coalesced (A/B against 1: profiles/r04/sorted_nt/ab_nt1_nt3.log)
+
 hipError_t launch_var_sorted(const VarLaunch& a, const void* img_g32, const void* img_g16, const void* img_g4,
                              const void* img_g8, hipStream_t stream) {
   const unsigned blocks = (unsigned)std::max<size_t>(1, a.max_blocks);
@@ -1196,17 +1210,31 @@ hipError_t launch_var_sorted(const VarLaunch& a, const void* img_g32, const void
                      static_cast<const uint4*>(a.img_slice), static_cast<const uint4*>(img_g32),               \
                      static_cast<const uint4*>(img_g16), static_cast<const uint4*>(img_g4),                    \
                      static_cast<const uint4*>(img_g8),                                                         \
-                     static_cast<const uint4*>(a.img_unshift), a.out)
-  static const bool nt = [] {
-    const char* e = std::getenv("ANNETY_CRC_SORTED_NT");
-    return !(e && e[0] == '0');
+                     static_cast<const uint4*>(a.img_unshift), a.out, classes)
+  static const uint32_t classes = [] {
+    const char* e = std::getenv("ANNETY_CRC_SORTED_CLASSES");
+    return e ? (uint32_t)std::atoi(e) & 7u : 7u;
   }();
-  if (a.update) {
-    if (nt) ANNETY_SORTED_LAUNCH(true, true);
-    else ANNETY_SORTED_LAUNCH(true, false);
-  } else {
-    if (nt) ANNETY_SORTED_LAUNCH(false, true);
-    else ANNETY_SORTED_LAUNCH(false, false);
+  static const int nt = [] {
+    const char* e = std::getenv("ANNETY_CRC_SORTED_NT");
+    return e && e[0] >= '0' && e[0] <= '7' ? e[0] - '0' : kSortedNtDefault;
+  }();
+  switch (nt) {
+#define ANNETY_SORTED_CASE(NT)                  \
+  case NT:                                      \
+    if (a.update) ANNETY_SORTED_LAUNCH(true, NT); \
+    else ANNETY_SORTED_LAUNCH(false, NT);       \
+    break;
+    ANNETY_SORTED_CASE(0)
+    ANNETY_SORTED_CASE(1)
+    ANNETY_SORTED_CASE(2)
+    ANNETY_SORTED_CASE(3)
+    ANNETY_SORTED_CASE(4)
+    ANNETY_SORTED_CASE(5)
+    ANNETY_SORTED_CASE(6)
+    ANNETY_SORTED_CASE(7)
+#undef ANNETY_SORTED_CASE
+    default: break;
   }
 #undef ANNETY_SORTED_LAUNCH
   return hipGetLastError();

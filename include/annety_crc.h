@@ -128,8 +128,9 @@ int annety_crc32_batch_fixed(const void* d_base, size_t n, size_t len, size_t st
 /* Variable length: payload i = [d_base + d_off[i], + d_len[i]) (any alignment).
  * Path choice is automatic. A recording call runs the extent kernel (a few us), which publishes the batch's
  * extent; once two completed recording calls on the same stream with the same (d_base, d_off, d_len, n) have
- * shown a dense, sorted batch (starts ascending, gaps < 4 KiB, payload bytes >= 2/3 of the span), calls take
- * the arena path over that span; otherwise (and for n < 1024) the length-sorted path. On the arena path one
+ * shown a dense batch (payload bytes >= 2/3 of the span) that is either sorted (starts ascending, gaps < 4 KiB)
+ * or lies inside one device allocation (any order, any gaps), calls take the arena path over that span;
+ * otherwise (and for n < 1024) the length-sorted path. On the arena path one
  * call in 8 records: it re-checks its own extent on the device and, if the layout changed under the same
  * pointers, folds every payload directly from its own bytes. The 7 calls in between skip the extent kernel
  * and the device check: the span is checked on the host to lie inside one device allocation (so the line
@@ -152,7 +153,7 @@ int annety_crc32_update_batch_var(uint32_t* d_state, const void* d_base, const u
 /* Arena variants of the two entry points above, for payloads that lie in one buffer of arena_bytes
  * bytes at d_arena (a NetBuffer's readable bytes, a frame stream, a packed batch; offsets are relative
  * to d_arena). One pass streams every 128-byte line of the arena whatever the length mix, then one lane
- * per payload joins its lines (DESIGN.md §2.8), so the cost follows arena_bytes: use these when the
+ * per payload joins its lines (DESIGN.md §2.6), so the cost follows arena_bytes: use these when the
  * payloads cover most of the arena, and the two entry points above for sparse batches. A payload that
  * reaches outside [0, arena_bytes) is still computed correctly (its lines are folded directly).
  * Same results and argument rules as annety_crc32_batch_var / annety_crc32_update_batch_var. */

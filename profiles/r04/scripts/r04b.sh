@@ -5,4 +5,4 @@ profiles/ab_run.sh r04b/ab_c3 ab/libannety_crc_4205b95.so 3 --config 3 --steps 2
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_c3 -o run -- python3 $GRAFT_REPO_ROOT/bench.py --config 3 --steps 100 --warmup 10 --no-cpu --sample-check > $O/kt_c3.log 2>&1
 cd $GRAFT_REPO_ROOT
-bash profiles/r04_scale_inputs.sh r04_scale
+bash profiles/r04/scripts/r04_scale_inputs.sh r04_scale
