@@ -701,13 +701,16 @@ __device__ __forceinline__ void var_class_nt(uint4* lds4, const uint8_t* __restr
       ln_g[g] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, g * G) << 32) |
                 (uint32_t)__builtin_amdgcn_readlane((int)lo, g * G);
     }
+    // branch-free (a scalar branch between two load sequences made the compiler drain the loads at the merge:
+    // 284 us against 222 per config-3 call): per group a scalar base at its payload's first line, per lane a
+    // 32-bit offset of its clamped line
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       const int g = G == 32 ? (i >> 1) & 1 : i & 3;
       const int piece = G == 32 ? 2 * (i >> 2) + (i & 1) : i >> 2;
       const int32_t rel = min(max(rel_g[g] + 8 * piece + (int32_t)(l & 7), 0), max_g[g]);
-      const uint64_t off = ((ln_g[g] + (uint64_t)rel) << 7) + chunk - b0;
-      const v4u32 x = __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(base + off));
+      const uint8_t* gb = base + ((ln_g[g] << 7) - b0);
+      const v4u32 x = __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(gb + ((uint32_t)rel * 128u + chunk)));
       v[i] = make_uint4(x.x, x.y, x.z, x.w);
     }
   };
@@ -991,7 +994,7 @@ __global__ __launch_bounds__(kBlock) void crc32_var_sorted_kernel(const uint8_t*
                                                                   uint32_t* __restrict__ out, uint32_t classes) {
   __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsVarImageBytes / 16];
   // classes: bit c runs class c (7 in the product; the microbench timing of one class alone leaves digests
-  // of the others unwritten, ANNETY_CRC_SORTED_CLASSES)
+  // of the others unwritten, ANNETY_CRC_SORTED_CLASSES); bit 3: the small class per line at G = 8, not 4
   if (classes & 1) {
     if constexpr (NT & 1)
       var_class_nt<32, UPD, 1>(lds4, base, desc, ranges, img_slice, img_g32, img_unshift, out);
@@ -1011,6 +1014,8 @@ __global__ __launch_bounds__(kBlock) void crc32_var_sorted_kernel(const uint8_t*
   if (!(classes & 4)) return;
   if constexpr (NT & 4)
     var_class_nt8<UPD>(lds4, base, desc, ranges + 4, img_slice, img_g8, out);
+  else if (classes & 8)  // (A/B: the small class per line at G = 8)
+    var_class<8, true, UPD, kVwg, 0, 0>(lds4, base, n, 0, 0, desc, ranges + 4, img_slice, img_g8, img_unshift, out);
   else
     var_class<4, true, UPD, kVwg, 0, 0>(lds4, base, n, 0, 0, desc, ranges + 4, img_slice, img_g4, img_unshift, out);
 }
@@ -1213,7 +1218,7 @@ hipError_t launch_var_sorted(const VarLaunch& a, const void* img_g32, const void
                      static_cast<const uint4*>(a.img_unshift), a.out, classes)
   static const uint32_t classes = [] {
     const char* e = std::getenv("ANNETY_CRC_SORTED_CLASSES");
-    return e ? (uint32_t)std::atoi(e) & 7u : 7u;
+    return e ? (uint32_t)std::atoi(e) & 15u : 7u;
   }();
   static const int nt = [] {
     const char* e = std::getenv("ANNETY_CRC_SORTED_NT");
