@@ -744,8 +744,19 @@ __device__ __forceinline__ void var_class_nt(uint4* lds4, const uint8_t* __restr
     const int32_t liA = (int32_t)(r_c * G + jA) - (int32_t)cur.vlead;
     const int32_t liB = liA + G / 2;
     const int32_t last = (int32_t)cur.nlines - 1;
-    if (liA < 2 || liA >= last) mask_half<UPD, 0>(v, liA, cur, l3);
-    if (liB < 2 || liB >= last) mask_half<UPD, 4>(v, liB, cur, l3);
+    // virtual lines of a first round: zeroed by selects (cheap); the payload's first, spill and last lines:
+    // the byte masks, on the one half-branch that holds them (a first round with both halves' general masks
+    // cost twice the VALU of the whole fold)
+    if (liA < 0 || liB < 0) {
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        v[i] = liA < 0 ? make_uint4(0u, 0u, 0u, 0u) : v[i];
+        v[4 + i] = liB < 0 ? make_uint4(0u, 0u, 0u, 0u) : v[4 + i];
+      }
+    }
+    const bool spill = cur.lead > 124 && cur.len >= 4;
+    if (liA == 0 || (liA == 1 && spill) || liA == last) mask_half<UPD, 0>(v, liA, cur, l3);
+    if (liB == 0 || (liB == 1 && spill) || liB == last) mask_half<UPD, 4>(v, liB, cur, l3);
     // the round register (shift_{(G-1)*128} of the lane's register, 0 at a payload's first round) enters the
     // first half of its line: lanes with l3 = 0 fold the first halves of their own line and of lane ^ 8's
     const uint32_t sin = nibble_map_uniform(s, lds, kLdsRoundOff);
@@ -790,8 +801,14 @@ __device__ __forceinline__ void var_class_nt(uint4* lds4, const uint8_t* __restr
   };
 
   auto step = [&](uint4 (&cur_buf)[8], uint4 (&nxt_buf)[8]) {
-    VarTask dec1 = decode_task<G>(d1, t1 < t_end);
-    if constexpr (UPD) dec1.state = dec1.valid ? out[dec1.p] : 0u;
+    // every group of the wave still in its task (r1 > 0): its descriptor is decoded already (no load in the
+    // branch, so the loads in flight are not drained at the merge; update mode decodes every step, since it
+    // loads the register there)
+    VarTask dec1 = dec0;
+    if (UPD || __builtin_amdgcn_ballot_w64(r1 == 0) != 0) {
+      dec1 = decode_task<G>(d1, t1 < t_end);
+      if constexpr (UPD) dec1.state = dec1.valid ? out[dec1.p] : 0u;
+    }
     const bool more = r1 + 1 < dec1.rounds;
     const size_t t2 = more ? t1 : t1 + ngroups;
     const uint32_t r2 = more ? r1 + 1 : 0u;
@@ -994,7 +1011,30 @@ __global__ __launch_bounds__(kBlock) void crc32_var_sorted_kernel(const uint8_t*
                                                                   uint32_t* __restrict__ out, uint32_t classes) {
   __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsVarImageBytes / 16];
   // classes: bit c runs class c (7 in the product; the microbench timing of one class alone leaves digests
-  // of the others unwritten, ANNETY_CRC_SORTED_CLASSES); bit 3: the small class per line at G = 8, not 4
+  // of the others unwritten, ANNETY_CRC_SORTED_CLASSES); bit 3: the small class per line at G = 8, not 4;
+  // bit 4: odd blocks run the classes in reverse order (small, G = 16, G = 32), so that the small class's
+  // latency-bound steps overlap other blocks' streaming instead of all blocks' tails
+  if ((classes & 16) && (blockIdx.x & 1)) {
+    if (classes & 4)
+      var_class<4, true, UPD, kVwg, 0, 1>(lds4, base, n, 0, 0, desc, ranges + 4, img_slice, img_g4, img_unshift, out);
+    else
+      load_image<kLdsVarImageBytes>(lds4, img_slice, img_g4, img_unshift);
+    __syncthreads();
+    if (classes & 2) {
+      if constexpr (NT & 2)
+        var_class_nt<16, UPD, 0>(lds4, base, desc, ranges + 2, img_slice, img_g16, img_unshift, out);
+      else
+        var_class<16, true, UPD, kVwg, 0, 0>(lds4, base, n, 0, 0, desc, ranges + 2, img_slice, img_g16, img_unshift, out);
+    }
+    __syncthreads();
+    if (classes & 1) {
+      if constexpr (NT & 1)
+        var_class_nt<32, UPD, 0>(lds4, base, desc, ranges, img_slice, img_g32, img_unshift, out);
+      else
+        var_class<32, true, UPD, kVwg, 0, 0>(lds4, base, n, 0, 0, desc, ranges, img_slice, img_g32, img_unshift, out);
+    }
+    return;
+  }
   if (classes & 1) {
     if constexpr (NT & 1)
       var_class_nt<32, UPD, 1>(lds4, base, desc, ranges, img_slice, img_g32, img_unshift, out);
@@ -1218,7 +1258,7 @@ hipError_t launch_var_sorted(const VarLaunch& a, const void* img_g32, const void
                      static_cast<const uint4*>(a.img_unshift), a.out, classes)
   static const uint32_t classes = [] {
     const char* e = std::getenv("ANNETY_CRC_SORTED_CLASSES");
-    return e ? (uint32_t)std::atoi(e) & 15u : 7u;
+    return e ? (uint32_t)std::atoi(e) & 31u : 7u;
   }();
   static const int nt = [] {
     const char* e = std::getenv("ANNETY_CRC_SORTED_NT");
