@@ -596,6 +596,7 @@ __device__ __forceinline__ void var_class(uint4* lds4, const uint8_t* __restrict
     d1 = d2;
   };
 
+  // (three buffers, two steps' loads in flight, measured no faster on the small class: DESIGN.md §7.2)
   while (dec0.valid) {
     step(A, B);
     step(B, A);  // harmless when the group ran out of work on the first half: nothing is stored
@@ -1010,8 +1011,8 @@ __global__ __launch_bounds__(kBlock) void crc32_var_sorted_kernel(const uint8_t*
                                                                   const uint4* __restrict__ img_unshift,
                                                                   uint32_t* __restrict__ out, uint32_t classes) {
   __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsVarImageBytes / 16];
-  // classes: bit c runs class c (7 in the product; the microbench timing of one class alone leaves digests
-  // of the others unwritten, ANNETY_CRC_SORTED_CLASSES); bit 3: the small class per line at G = 8, not 4;
+  // classes: bit c runs class c (the product runs all three; the microbench timing of one class alone leaves
+  // digests of the others unwritten, ANNETY_CRC_SORTED_CLASSES); bit 3: the small class per line at G = 8, not 4;
   // bit 4: odd blocks run the classes in reverse order (small, G = 16, G = 32), so that the small class's
   // latency-bound steps overlap other blocks' streaming instead of all blocks' tails
   if ((classes & 16) && (blockIdx.x & 1)) {
@@ -1243,6 +1244,8 @@ hipError_t launch_fixed(const FixedLaunch& a, hipStream_t stream) {
   return a.full ? launch_full<true, false>(a, stream) : launch_full<false, false>(a, stream);
 }
 
+// the three classes, odd blocks in reverse order (A/B against 7: profiles/r04/sorted_nt/ab_class_order.log)
+constexpr uint32_t kSortedClassesDefault = 23;
 constexpr int kSortedNtDefault = 3;  // crc32_var_sorted_kernel NT: G = 32 and G = 16 coalesced (A/B against 1: profiles/r04/sorted_nt/ab_nt1_nt3.log)
 
 hipError_t launch_var_sorted(const VarLaunch& a, const void* img_g32, const void* img_g16, const void* img_g4,
@@ -1258,7 +1261,7 @@ hipError_t launch_var_sorted(const VarLaunch& a, const void* img_g32, const void
                      static_cast<const uint4*>(a.img_unshift), a.out, classes)
   static const uint32_t classes = [] {
     const char* e = std::getenv("ANNETY_CRC_SORTED_CLASSES");
-    return e ? (uint32_t)std::atoi(e) & 31u : 7u;
+    return e ? (uint32_t)std::atoi(e) & 31u : kSortedClassesDefault;
   }();
   static const int nt = [] {
     const char* e = std::getenv("ANNETY_CRC_SORTED_NT");
