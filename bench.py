@@ -43,6 +43,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.
 # Per-launch HBM bytes from the rocprofv3 PMC passes of this bench's own command (profiles/pmc.sh, FETCH_SIZE x2
 # gfx950 correction + WRITE_SIZE), committed per config; reported as `traffic` with the file as its source
 # (a PMC pass cannot run inside the timed process).
+PMC_FILES_VAR = {"sorted": "profiles/r04/config3_sorted_pmc.json"}  # config 3 on another variable path
 PMC_FILES = {1: "profiles/r04/config1_pmc.json", 3: "profiles/r04/config3_pmc.json",
              2: "profiles/r04/config2_pmc.json", 4: "profiles/r04/config1_pmc.json"}
 CPU_SAMPLE_BYTES = 1 << 30  # cpu_baseline sample: up to 1 GiB of the workload, far above the host's caches
@@ -365,7 +366,9 @@ def pmc_traffic(w: Workload, var_path: str):
     (profiles/pmc.sh + pmc.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), summed over the kernels
     of one step, or None if no summary for this configuration is committed."""
     path = PMC_FILES.get(w.config)
-    if not path or (w.config == 3 and var_path != "arena") or (w.config in (1, 4) and w.L != 1024):
+    if w.config == 3 and var_path != "arena":
+        path = PMC_FILES_VAR.get(var_path)
+    if not path or (w.config in (1, 4) and w.L != 1024):
         return None
     try:
         with open(os.path.join(ROOT, path)) as f:
