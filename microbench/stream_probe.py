@@ -10,7 +10,7 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def child(which: str, reps: int = 50):
+def child(which: str, reps: int = int(os.environ.get("REPS", "50"))):
     probe = int(which) if which.isdigit() else -1
     sys.path.insert(0, ROOT)
     import numpy as np
@@ -62,7 +62,7 @@ def child(which: str, reps: int = 50):
         ok = bool(np.array_equal(out.cpu().numpy().view(np.uint32), want))
     import time
 
-    t_end = time.time() + 1.0  # clocks up (the bench's --prewarm-s)
+    t_end = time.time() + float(os.environ.get("PREWARM_S", "1.0"))  # clocks up (the bench's --prewarm-s)
     while time.time() < t_end:
         for _ in range(20):
             fn(*args)
