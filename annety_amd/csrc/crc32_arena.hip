@@ -416,50 +416,11 @@ __global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchGeo g0, c
   const size_t p_first = (size_t)blockIdx.x * per + threadIdx.x;
   Plan y{};
   Vals v{};
-  if (PIPE != 3 && p_first < p_end) {
+  if (p_first < p_end) {
     st.plan_a(p_first, y, v);
     st.plan_b(p_first, y, v);
   }
-  if constexpr (PIPE == 3) {
-    // PIPE 1 with every descriptor fetched one iteration before its plan and every load unconditional (indices
-    // clamped to the block's last payload): in PIPE 1 a plan loads its descriptor and needs it at once, and
-    // waiting for the newest load also drains every older one, the other payload's window and S/SB loads
-    const size_t last = p_end > 0 ? p_end - 1 : 0;
-    auto cl = [&](size_t q) { return q < p_end ? q : last; };
-    Plan y2{};
-    Vals v2{};
-    {
-      const size_t q0 = cl(p_first), q1 = cl(p_first + BLK);
-      const uint32_t l0 = g.len[q0], l1 = g.len[q1];
-      const uint64_t o0 = g.off[q0], o1 = g.off[q1];
-      st.plan_a(q0, l0, o0, y, v);
-      st.plan_b(q0, y, v);
-      st.plan_a(q1, l1, o1, y2, v2);
-      st.plan_b(q1, y2, v2);
-    }
-    size_t qa = cl(p_first + 2 * BLK), qb = cl(p_first + 3 * BLK);
-    uint32_t la = g.len[qa], lb = g.len[qb];
-    uint64_t oa = g.off[qa], ob = g.off[qb];
-    load_image<kLdsStitchImageBytes, BLK, kLdsCommonBytes>(lds4, img_slice, nullptr, img_stitch);
-    __syncthreads();
-    for (size_t p = p_first; p < p_end; p += 2 * BLK) {
-      const size_t qa2 = cl(p + 4 * BLK), qb2 = cl(p + 5 * BLK);
-      const uint32_t la2 = g.len[qa2], lb2 = g.len[qb2];
-      const uint64_t oa2 = g.off[qa2], ob2 = g.off[qb2];
-      st.process(p, y, v);
-      st.plan_a(qa, la, oa, y, v);
-      st.plan_b(qa, y, v);
-      if (p + BLK < p_end) st.process(p + BLK, y2, v2);
-      st.plan_a(qb, lb, ob, y2, v2);
-      st.plan_b(qb, y2, v2);
-      qa = qa2;
-      qb = qb2;
-      la = la2;
-      lb = lb2;
-      oa = oa2;
-      ob = ob2;
-    }
-  } else if constexpr (PIPE == 1) {
+  if constexpr (PIPE == 1) {
     Plan y2{};
     Vals v2{};
     if (p_first + BLK < p_end) {
@@ -820,9 +781,9 @@ hipError_t launch_arena(const ArenaLaunch& a, hipStream_t stream) {
   // (profiles/r02/stitch_pipe_bench_ab/). ANNETY_CRC_STITCH_PIPE=0 selects the one-payload-at-a-time loop.
   // 768-lane blocks with one payload in flight (3 waves per SIMD under a 168-VGPR cap, no spill) measured
   // 21.3 us against 20.4 for this 512-lane form (profiles/r03/stitch_ab/): occupancy is not what bounds it.
-  static const int pipe = [] {
+  static const bool pipe = [] {
     const char* e = std::getenv("ANNETY_CRC_STITCH_PIPE");
-    return e && (e[0] == '0' || e[0] == '3') ? e[0] - '0' : 1;
+    return !(e && e[0] == '0');
   }();
   // ANNETY_CRC_STITCH_MID=1: the one-level superblock join (mid_level), which fits the VGPRs only without PIPE
   static const bool mid = [] {
@@ -830,7 +791,6 @@ hipError_t launch_arena(const ArenaLaunch& a, hipStream_t stream) {
     return e && e[0] == '1';
   }();
   if (mid) return launch_stitch_p<0, 0, kStitchBlock, true>(a, stream);
-  if (pipe == 3) return launch_stitch_p<0, 3>(a, stream);
   return pipe ? launch_stitch_p<0, 1>(a, stream) : launch_stitch_p<0>(a, stream);
 }
 
