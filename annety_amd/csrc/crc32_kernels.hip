@@ -1029,9 +1029,7 @@ __global__ __launch_bounds__(kBlock) void crc32_var_sorted_kernel(const uint8_t*
     }
     __syncthreads();
     if (classes & 1) {
-      if (classes & 64)
-        var_class_nt<16, UPD, 0>(lds4, base, desc, ranges, img_slice, img_g16, img_unshift, out);
-      else if constexpr (NT & 1)
+      if constexpr (NT & 1)
         var_class_nt<32, UPD, 0>(lds4, base, desc, ranges, img_slice, img_g32, img_unshift, out);
       else
         var_class<32, true, UPD, kVwg, 0, 0>(lds4, base, n, 0, 0, desc, ranges, img_slice, img_g32, img_unshift, out);
@@ -1039,9 +1037,7 @@ __global__ __launch_bounds__(kBlock) void crc32_var_sorted_kernel(const uint8_t*
     return;
   }
   if (classes & 1) {
-    if (classes & 64)  // (A/B: the >= 128-line class at G = 16)
-      var_class_nt<16, UPD, 1>(lds4, base, desc, ranges, img_slice, img_g16, img_unshift, out);
-    else if constexpr (NT & 1)
+    if constexpr (NT & 1)
       var_class_nt<32, UPD, 1>(lds4, base, desc, ranges, img_slice, img_g32, img_unshift, out);
     else
       var_class<32, true, UPD, kVwg, 0, 1>(lds4, base, n, 0, 0, desc, ranges, img_slice, img_g32, img_unshift, out);
@@ -1265,7 +1261,7 @@ hipError_t launch_var_sorted(const VarLaunch& a, const void* img_g32, const void
                      static_cast<const uint4*>(a.img_unshift), a.out, classes)
   static const uint32_t classes = [] {
     const char* e = std::getenv("ANNETY_CRC_SORTED_CLASSES");
-    return e ? (uint32_t)std::atoi(e) & 127u : kSortedClassesDefault;
+    return e ? (uint32_t)std::atoi(e) & 31u : kSortedClassesDefault;
   }();
   static const int nt = [] {
     const char* e = std::getenv("ANNETY_CRC_SORTED_NT");
