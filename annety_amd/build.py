@@ -15,7 +15,7 @@ ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(ROOT, "include")
 LIB = os.path.join(PKG, "libannety_crc.so")
-SOURCES = ["crc32_kernels.hip", "crc32_arena.hip", "crc32_stream.hip", "crc32_frames.hip", "crc32_host.cpp", "crc32_capi.cpp",
+SOURCES = ["crc32_kernels.hip", "crc32_arena.hip", "crc32_frames.hip", "crc32_host.cpp", "crc32_capi.cpp",
            "crc32_group.cpp"]
 HEADERS = ["crc32_kernels.h", "crc32_math.h", "crc32_device.h", "crc32_arena_lines.h", "crc32_host.h"]
 ARCH = "gfx950"

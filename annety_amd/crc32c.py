@@ -113,13 +113,13 @@ def scratch_stats(device: int = 0) -> dict:
     return {"slots": v[0].value, "handoffs": v[1].value, "device_syncs": v[2].value}
 
 
-VAR_PATHS = {"auto": 0, "sorted": 1, "stream": 2}
+VAR_PATHS = {"auto": 0, "sorted": 1}
 
 
 def set_var_path(path: str) -> str:
     """annety_crc_set_var_path: the path of crc32_batch_var / crc32_update_batch_var, process-wide ("auto" =
-    arena or length-sorted from recorded extents, "sorted", "stream" = the line stream). Returns the previous
-    path. Digests do not depend on it."""
+    arena or length-sorted from recorded extents, "sorted"). Returns the previous path. Digests do not depend
+    on it."""
     lib = _lib.get()
     prev = {v: k for k, v in VAR_PATHS.items()}[lib.annety_crc_get_var_path()]
     _lib.check(lib.annety_crc_set_var_path(VAR_PATHS[path]), "annety_crc_set_var_path")

@@ -59,7 +59,7 @@ __device__ __forceinline__ uint32_t seg_map(uint32_t t, uint32_t idx, const uint
   return nibble_map_set<32>(t, lds, kLdsMapOff, idx);
 }
 // P(c) = shift_{c*8KiB} for a lane-varying c in 1..7: G(8) of the segment set for c = 1, else the mid set
-__device__ __forceinline__ uint32_t mid_map(uint32_t t, uint32_t c, const uint32_t* lds) {
+[[maybe_unused]] __device__ __forceinline__ uint32_t mid_map(uint32_t t, uint32_t c, const uint32_t* lds) {
   const bool one = c == 1;
   const uint32_t* b = lds + (one ? kLdsMapOff / 4 + (kMapG + 7) * 16 : kLdsMidOff / 4 + (c - 2) * 16);
   const uint32_t stride = one ? 32 * 16 : kMidMaps * 16;
@@ -761,14 +761,14 @@ hipError_t launch_arena_lines_p(const ArenaLaunch& a, hipStream_t stream) {
   return hipGetLastError();
 }
 
-// The line pass reads each superblock as 8 coalesced nontemporal 1 KiB loads (crc32_arena_lines.h);
-// ANNETY_CRC_LINES_NT=0 selects the per-line loads (A/B), read once.
+// The line pass reads each superblock as 8 coalesced nontemporal 1 KiB loads (crc32_arena_lines.h); A/B builds
+// select the per-line loads with ANNETY_CRC_LINES_NT=0.
 hipError_t launch_arena_lines(const ArenaLaunch& a, hipStream_t stream) {
-  static const bool nt = [] {
-    const char* e = std::getenv("ANNETY_CRC_LINES_NT");
-    return !(e && e[0] == '0');
-  }();
-  return nt ? launch_arena_lines_p<0, true>(a, stream) : launch_arena_lines_p<0, false>(a, stream);
+#ifdef ANNETY_CRC_AB
+  static const bool nt = ANNETY_AB_KNOB("ANNETY_CRC_LINES_NT", 1) != 0;
+  if (!nt) return launch_arena_lines_p<0, false>(a, stream);
+#endif
+  return launch_arena_lines_p<0, true>(a, stream);
 }
 
 hipError_t launch_arena(const ArenaLaunch& a, hipStream_t stream) {
@@ -778,20 +778,18 @@ hipError_t launch_arena(const ArenaLaunch& a, hipStream_t stream) {
   }
   // The stitch issues a lane's next payload loads before folding the current one (PIPE 1): config-3 step
   // 0.2139-0.2142 ms vs 0.2144-0.2151 without, same box, three alternating pairs
-  // (profiles/r02/stitch_pipe_bench_ab/). ANNETY_CRC_STITCH_PIPE=0 selects the one-payload-at-a-time loop.
-  // 768-lane blocks with one payload in flight (3 waves per SIMD under a 168-VGPR cap, no spill) measured
-  // 21.3 us against 20.4 for this 512-lane form (profiles/r03/stitch_ab/): occupancy is not what bounds it.
-  static const bool pipe = [] {
-    const char* e = std::getenv("ANNETY_CRC_STITCH_PIPE");
-    return !(e && e[0] == '0');
-  }();
-  // ANNETY_CRC_STITCH_MID=1: the one-level superblock join (mid_level), which fits the VGPRs only without PIPE
-  static const bool mid = [] {
-    const char* e = std::getenv("ANNETY_CRC_STITCH_MID");
-    return e && e[0] == '1';
-  }();
+  // (profiles/r02/stitch_pipe_bench_ab/). 768-lane blocks with one payload in flight (3 waves per SIMD under a
+  // 168-VGPR cap, no spill) measured 21.3 us against 20.4 for this 512-lane form (profiles/r03/stitch_ab/):
+  // occupancy is not what bounds it. A/B builds: ANNETY_CRC_STITCH_PIPE=0 (one payload at a time),
+  // ANNETY_CRC_STITCH_MID=1 (the one-level superblock join, which fits the VGPRs only without PIPE; measured
+  // no faster).
+#ifdef ANNETY_CRC_AB
+  static const bool pipe = ANNETY_AB_KNOB("ANNETY_CRC_STITCH_PIPE", 1) != 0;
+  static const bool mid = ANNETY_AB_KNOB("ANNETY_CRC_STITCH_MID", 0) == 1;
   if (mid) return launch_stitch_p<0, 0, kStitchBlock, true>(a, stream);
-  return pipe ? launch_stitch_p<0, 1>(a, stream) : launch_stitch_p<0>(a, stream);
+  if (!pipe) return launch_stitch_p<0>(a, stream);
+#endif
+  return launch_stitch_p<0, 1>(a, stream);
 }
 
 }  // namespace annety_crc

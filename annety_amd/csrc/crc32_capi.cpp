@@ -83,7 +83,6 @@ struct HostImages {
   std::vector<uint32_t> unshift; // 24 maps x 128 words (U_lo[0..15], U_hi[0..7])
   std::vector<uint32_t> sb;      // arena superblock join: (k, v, g) = shift_{(7-g)*1024}(v << 4k); byte map
   std::vector<uint32_t> stitch;  // arena stitch: segment maps F/G/UL/UB, unshift, shift_32 (crc32_math.h)
-  std::vector<uint32_t> stream;  // line-stream path: scan maps, U sets, power maps (crc32_math.h)
 };
 
 // Apply matrix m to (v << 4k) for every nibble value: the 16-entry table of one nibble position.
@@ -211,18 +210,6 @@ const HostImages& host_images() {
       for (uint32_t c = 2; c < 2 + kMidMaps; c++) nibble_tables(shift_matrix((uint64_t)8192 * c), mid.data() + (c - 2) * 128);
       put_set(m + (kLdsMidOff - kLdsMapOff) / 4, mid.data(), kMidMaps);
     }
-    img.stream.assign(kStreamImgBytes / 4, 0);
-    {
-      uint32_t* m = img.stream.data();
-      put_set(m + kStreamULoOff / 4, img.unshift.data(), 16);
-      put_set(m + kStreamUHiOff / 4, img.unshift.data() + 16 * 128, 8);
-      for (uint32_t a = 0; a < 128; a++) m[kStreamInitOff / 4 + a] = shift_bits(kInit, 8u * (128 - a));
-      for (uint32_t i = 0; i < 6; i++) nibble_tables(shift_matrix((uint64_t)kChunkBytes << i), m + (kStreamPowOff + 512 * i) / 4);
-      for (uint32_t i = 0; i < 32; i++) {
-        const Gf2Mat g = shift_matrix((uint64_t)kChunkBytes << i);
-        std::memcpy(m + kStreamMatOff / 4 + 32 * i, g.col, sizeof g.col);
-      }
-    }
   });
   return img;
 }
@@ -271,13 +258,6 @@ struct Scratch {
   uint64_t since_extent = 0;              // arena calls since the last one that recorded its extent
   uint64_t seen_seq = 0, prev_seq = 0;    // the two latest completed hints read for this key
   ExtentHint seen{}, prev{};
-  // line-stream path (run_var_stream): the scan's two look-back status sets, alternating per call; each call
-  // zeroes the records the previous one left in the other set
-  uint64_t* st = nullptr;  // 2 sets of st_set_words words
-  size_t st_set_words = 0;
-  uint64_t st_calls = 0;            // set (st_calls & 1) is the next call's
-  uint32_t st_used[2] = {0, 0};     // tiles the latest call on each set wrote (0: the set is zero)
-  bool st_clean = false;            // both sets zero (false after an allocation or a failed launch)
 };
 using ScratchSlot = host::Slot<Scratch>;
 
@@ -324,7 +304,6 @@ struct DeviceCtx {
   uint32_t* d_unshift = nullptr;
   void* d_sb = nullptr;
   void* d_stitch = nullptr;
-  void* d_stream_img = nullptr;
   void* d_zero = nullptr;  // 256 zero bytes
   Staging stg;
   std::mutex stg_mu;  // one host-staged batch at a time per device
@@ -349,12 +328,12 @@ size_t grid_cus(const DeviceCtx& c) { return (size_t)std::max(1, c.cus - g_reser
 std::mutex g_init_mu;
 
 void free_images(DeviceCtx& c) {
-  void* bufs[] = {c.d_slice, c.d_groups, c.d_unshift, c.d_sb, c.d_stitch, c.d_stream_img, c.d_zero};
+  void* bufs[] = {c.d_slice, c.d_groups, c.d_unshift, c.d_sb, c.d_stitch, c.d_zero};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   c.d_slice = c.d_groups = nullptr;
   c.d_unshift = nullptr;
-  c.d_sb = c.d_stitch = c.d_stream_img = c.d_zero = nullptr;
+  c.d_sb = c.d_stitch = c.d_zero = nullptr;
 }
 
 int init_device_locked(int dev) {
@@ -378,8 +357,6 @@ int init_device_locked(int dev) {
     if ((e = hipMalloc(&c.d_unshift, img.unshift.size() * 4)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMalloc(&c.d_sb, img.sb.size() * 4)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMalloc(&c.d_stitch, img.stitch.size() * 4)) != hipSuccess) { rc = hip_fail(e); break; }
-    if ((e = hipMalloc(&c.d_stream_img, img.stream.size() * 4)) != hipSuccess) { rc = hip_fail(e); break; }
-    if ((e = hipMemcpy(c.d_stream_img, img.stream.data(), img.stream.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMalloc(&c.d_zero, 256)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMemset(c.d_zero, 0, 256)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMemcpy(c.d_sb, img.sb.data(), img.sb.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_fail(e); break; }
@@ -541,12 +518,9 @@ size_t sorted_scratch_bytes(size_t n) {
   return (rows_words + 8) * sizeof(uint32_t) + 16 * n;  // rows + ranges (16-byte multiple) + descriptors
 }
 
-// The length classes in one launch (1, default) or one launch each (ANNETY_CRC_SORTED_FUSED=0). Read once.
+// The length classes in one launch (the product) or one launch each (A/B builds: ANNETY_CRC_SORTED_FUSED=0).
 bool sorted_fused() {
-  static const bool on = [] {
-    const char* e = std::getenv("ANNETY_CRC_SORTED_FUSED");
-    return !(e && e[0] == '0');
-  }();
+  static const bool on = ANNETY_AB_KNOB("ANNETY_CRC_SORTED_FUSED", 1) != 0;
   return on;
 }
 
@@ -795,79 +769,11 @@ int run_var_auto(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_o
   return rc ? rc : rd;
 }
 
-// ---- line-stream path (crc32_stream.hip): any layout, no sort ----
-// Scratch inside the slot: desc (16 B per payload), posv (8 B), edges (8 B), totals, pieces (16 B per stream wave)
-// and join counters (4 B per stream wave).
-size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
-size_t stream_scratch_bytes(size_t n, size_t waves) {
-  return align256(16 * n) + 2 * align256(8 * n) + 256 + 16 * waves + 4 * waves;
-}
-
-int run_var_stream(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_off, const uint32_t* d_len,
-                   uint32_t* d_out, hipStream_t stream, bool update) {
-  const size_t blocks = grid_cus(c), waves = blocks * (size_t)(fixed_kernel_block() / 64);
-  std::lock_guard<std::mutex> lk(c.arena_mu);
-  ScratchSlot* slot = nullptr;
-  int rc = scratch_slot(c, stream, stream_scratch_bytes(n, waves), &slot);
-  if (rc) return rc;
-  Scratch& d = slot->data;
-  const uint32_t ntiles = (uint32_t)((n + kStreamTile - 1) / kStreamTile);
-  const size_t set_words = kStreamSetHeader + (size_t)kStreamRecWords * ntiles;
-  if (d.st_set_words < set_words) {  // grown in stream order, like the slot's scratch
-    if (d.st) HIP_TRY(hipFreeAsync(d.st, stream));
-    d.st = nullptr;
-    d.st_set_words = 0;
-    HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&d.st), 2 * set_words * sizeof(uint64_t), stream));
-    d.st_set_words = set_words;
-    d.st_clean = false;
-  }
-  if (!d.st_clean) {
-    HIP_TRY(hipMemsetAsync(d.st, 0, 2 * d.st_set_words * sizeof(uint64_t), stream));
-    d.st_clean = true;
-    d.st_used[0] = d.st_used[1] = 0;
-  }
-  const uint32_t set = (uint32_t)(d.st_calls & 1);
-  char* sc = path_scratch(slot);
-  StreamLaunch a{};
-  a.base = d_base;
-  a.off = d_off;
-  a.len = d_len;
-  a.n = n;
-  a.out = d_out;
-  a.update = update;
-  a.desc = sc;
-  a.posv = reinterpret_cast<uint64_t*>(sc + align256(16 * n));
-  a.edges = reinterpret_cast<uint32_t*>(sc + align256(16 * n) + align256(8 * n));
-  a.totals = reinterpret_cast<uint64_t*>(sc + align256(16 * n) + 2 * align256(8 * n));
-  a.pieces = reinterpret_cast<uint4*>(sc + align256(16 * n) + 2 * align256(8 * n) + 256);
-  a.counters = reinterpret_cast<uint32_t*>(sc + align256(16 * n) + 2 * align256(8 * n) + 256 + 16 * waves);
-  a.status = d.st + set * d.st_set_words;
-  a.status_other = d.st + (set ^ 1) * d.st_set_words;
-  a.other_words = d.st_used[set ^ 1] ? kStreamSetHeader + (size_t)kStreamRecWords * d.st_used[set ^ 1] : 0;
-  a.ntiles = ntiles;
-  a.img_slice = c.d_slice;
-  a.img_stream = c.d_stream_img;
-  a.zero_line = c.d_zero;
-  a.max_blocks = blocks;
-  const hipError_t e = launch_stream(a, stream);
-  if (e != hipSuccess) {
-    d.st_clean = false;  // a set may hold records: the next call zeroes both
-    rc = hip_fail(e);
-  } else {
-    d.st_used[set] = ntiles;
-    d.st_used[set ^ 1] = 0;
-    d.st_calls++;
-  }
-  const int rd = scratch_done(c, slot);
-  return rc ? rc : rd;
-}
-
-// The general variable path (annety_crc_set_var_path; initial value from ANNETY_CRC_VAR_PATH = auto / sorted /
-// stream, or ANNETY_CRC_VAR_AUTO=0 = sorted): 0 = automatic arena/sorted choice from recorded extents,
-// 1 = the length-sorted path, 2 = the line stream.
+// The general variable path (annety_crc_set_var_path; initial value from ANNETY_CRC_VAR_PATH = auto / sorted,
+// or ANNETY_CRC_VAR_AUTO=0 = sorted): 0 = automatic arena/sorted choice from recorded extents, 1 = the
+// length-sorted path.
 std::atomic<int> g_var_mode{[] {
   const char* e = std::getenv("ANNETY_CRC_VAR_PATH");
-  if (e && std::strcmp(e, "stream") == 0) return 2;
   if (e && std::strcmp(e, "sorted") == 0) return 1;
   if (e && std::strcmp(e, "auto") == 0) return 0;
   const char* a = std::getenv("ANNETY_CRC_VAR_AUTO");
@@ -877,7 +783,6 @@ std::atomic<int> g_var_mode{[] {
 int run_var_any(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_off, const uint32_t* d_len,
                 uint32_t* d_out, hipStream_t stream, bool update) {
   switch (g_var_mode.load(std::memory_order_relaxed)) {
-    case 2: return run_var_stream(c, d_base, n, d_off, d_len, d_out, stream, update);
     case 1: return run_var_sorted(c, d_base, n, d_off, d_len, d_out, stream, update);
     default: return run_var_auto(c, d_base, n, d_off, d_len, d_out, stream, update);
   }
@@ -1035,7 +940,6 @@ int annety_crc_shutdown(void) {
       HipSlotOps ops;
       c.slots.clear(ops, [](ScratchSlot& sl) {
         if (sl.data.ptr) (void)hipFree(sl.data.ptr);
-        if (sl.data.st) (void)hipFree(sl.data.st);
         if (sl.data.hint) (void)hipHostFree(sl.data.hint);
       });
     }
@@ -1073,7 +977,7 @@ int annety_crc_scratch_stats(int device, uint64_t* slots, uint64_t* handoffs, ui
 }
 
 int annety_crc_set_var_path(int mode) {
-  if (mode < 0 || mode > 2) return ANNETY_CRC_EINVAL;
+  if (mode < 0 || mode > 1) return ANNETY_CRC_EINVAL;
   g_var_mode.store(mode);
   return ANNETY_CRC_OK;
 }
@@ -1096,14 +1000,23 @@ int annety_crc_stream_release(void* stream) {
   std::lock_guard<std::mutex> lk(c->arena_mu);
   HipSlotOps ops;
   return c->slots.release(ops, s, s == hipStreamPerThread, [&](ScratchSlot& sl) -> int {
+    // Every member is released even when a step fails (the slot leaves the table either way), and the first
+    // failure is returned (an early return leaked the pinned record).
+    int first = ANNETY_CRC_OK;
+    auto note = [&](hipError_t e) {
+      if (e != hipSuccess && first == ANNETY_CRC_OK) first = hip_fail(e);
+    };
     // stream-ordered: the memory returns to the pool after the stream's queued work, nobody waits
-    if (sl.data.ptr) HIP_TRY(hipFreeAsync(sl.data.ptr, s));
-    if (sl.data.st) HIP_TRY(hipFreeAsync(sl.data.st, s));
+    if (sl.data.ptr) note(hipFreeAsync(sl.data.ptr, s));
+    sl.data.ptr = nullptr;
     if (sl.data.hint) {  // the stream's queued extent kernels may still write it: wait for them first
-      HIP_TRY(hipStreamSynchronize(s));
+      const hipError_t e = hipStreamSynchronize(s);
+      note(e);
+      if (e != hipSuccess) (void)hipDeviceSynchronize();  // nothing may still write it when it goes
       (void)hipHostFree(sl.data.hint);
+      sl.data.hint = nullptr;
     }
-    return ANNETY_CRC_OK;
+    return first;
   });
 }
 

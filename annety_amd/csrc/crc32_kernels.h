@@ -5,6 +5,21 @@
 #include <stddef.h>
 #include <stdint.h>
 
+// A/B switches of the design-space harnesses (microbench/): the environment is read only in builds compiled
+// with -DANNETY_CRC_AB. The product library always runs the measured defaults, so no environment variable can
+// change a digest or a kernel choice (probe modes that wrote wrong digests were reachable from the
+// environment). ANNETY_AB_KNOB(name, default) is the integer value of environment variable `name`.
+#ifdef ANNETY_CRC_AB
+#include <cstdlib>
+#define ANNETY_AB_KNOB(name, dflt)                 \
+  ([]() -> int {                                   \
+    const char* e_ = std::getenv(name);            \
+    return e_ && *e_ ? std::atoi(e_) : (int)(dflt); \
+  }())
+#else
+#define ANNETY_AB_KNOB(name, dflt) ((int)(dflt))
+#endif
+
 namespace annety_crc {
 
 struct ShiftCols {
@@ -187,66 +202,6 @@ inline ArenaGeom arena_geom(const ArenaLaunch& a) {
   if (want > a.max_blocks) want = a.max_blocks;
   return arena_geom(a, (size_t)want);
 }
-
-// Line-stream path (crc32_stream.hip): scan + stream launches, no host round trip. Scratch: desc (16 B), posv
-// (8 B) and edges (8 B) per payload, totals (4 words), pieces (16 B) and a join counter (4 B) per wave of the
-// stream launch, and two
-// alternating status sets of the scan's look-back (kStreamSetHeader + kStreamRecWords words per tile).
-constexpr uint32_t kStreamTile = 2048;      // payloads per scan tile
-constexpr uint32_t kStreamSetHeader = 8;    // words: [0] the ticket counter
-constexpr uint32_t kStreamRecWords = 8;     // words per tile record
-struct StreamScanArgs {
-  const uint8_t* base;
-  const uint64_t* off;
-  const uint32_t* len;
-  size_t n;
-  uint32_t* out;          // empty payloads' digests (crc32_long mode)
-  uint4* desc;            // {addr lo, addr hi, len, index} of the k-th non-empty payload
-  uint64_t* posv;         // its first position (line of the stream)
-  uint64_t* totals;       // [0] non-empty payloads K, [1] positions, [2] nonzero = a look-back gave up
-  uint64_t* status;       // this call's set (zero on entry)
-  uint64_t* other;        // the previous call's set: zeroed here, other_words words
-  size_t other_words;
-  uint32_t ntiles;
-  uint32_t* counters;     // the stream launch's join counters (one per wave), zeroed here
-  size_t ncounters;
-};
-struct StreamArgs {       // the stream launch (crc32_stream.hip)
-  const uint4* desc;
-  const uint64_t* posv;
-  const uint64_t* totals;
-  uint32_t* edges;
-  uint32_t* out;
-  uint4* pieces;
-  uint32_t* counters;
-  const uint8_t* zero_line;
-  const uint4* img_slice;
-  const uint4* img_stream;
-  const uint32_t* mats;   // the power matrices (img_stream + kStreamMatOff)
-};
-struct StreamLaunch {
-  const void* base;
-  const uint64_t* off;
-  const uint32_t* len;
-  size_t n;
-  uint32_t* out;          // digests, or (update) registers in place
-  bool update;
-  void* desc;
-  uint64_t* posv;
-  uint64_t* totals;
-  uint32_t* edges;        // 2 words per non-empty payload: its first and last line's masked CRC
-  uint4* pieces;          // 8 * max_blocks entries
-  uint32_t* counters;     // 8 * max_blocks entries
-  uint64_t* status;
-  uint64_t* status_other;
-  size_t other_words;
-  uint32_t ntiles;        // ceil(n / kStreamTile)
-  const void* img_slice;  // common image part
-  const void* img_stream; // kStreamImgBytes (crc32_math.h): the LDS part, then the power matrices
-  const void* zero_line;  // 128 zero bytes (device)
-  size_t max_blocks;      // stream launch grid (one workgroup per CU)
-};
-hipError_t launch_stream(const StreamLaunch& a, hipStream_t stream);
 
 hipError_t launch_arena(const ArenaLaunch& a, hipStream_t stream);
 // the line pass alone (crc32_arena.hip, crc32_arena_lines.h)

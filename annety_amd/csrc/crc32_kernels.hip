@@ -652,7 +652,7 @@ template <bool UPD, int O>
 __device__ __forceinline__ void mask_half(uint4 (&v)[8], int32_t li, const VarTask& cur, uint32_t h) {
   apply_half_mask<UPD, O>(v, half_mask<UPD>(li, cur), h);
 }
-__device__ __forceinline__ int32_t lane_xor8(int32_t x) { return __builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, false); }
+[[maybe_unused]] __device__ __forceinline__ int32_t lane_xor8(int32_t x) { return __builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, false); }
 
 // The G = 32 and G = 16 length classes with coalesced nontemporal loads (crc32_fixed32_nt_kernel's access
 // shape on the sorted descriptors). A wave holds NG = 64 / G lane groups, each stepping through its own
@@ -1180,13 +1180,10 @@ hipError_t launch_one_g(const FixedLaunch& a, hipStream_t stream) {
   return hipGetLastError();
 }
 
-// ANNETY_CRC_FIXED_NT=0 keeps contiguous 1 KiB batches on crc32_oneround_kernel<8> and G = 32 batches on
-// crc32_fixed_kernel<32> (A/B), read once.
+// A/B builds only (ANNETY_CRC_FIXED_NT=0): contiguous 1 KiB batches on crc32_oneround_kernel<8> and G = 32
+// batches on crc32_fixed_kernel<32>. Read once.
 bool onekib_nt_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("ANNETY_CRC_FIXED_NT");
-    return !(e && e[0] == '0');
-  }();
+  static const bool on = ANNETY_AB_KNOB("ANNETY_CRC_FIXED_NT", 1) != 0;
   return on;
 }
 
@@ -1259,31 +1256,9 @@ hipError_t launch_var_sorted(const VarLaunch& a, const void* img_g32, const void
                      static_cast<const uint4*>(img_g16), static_cast<const uint4*>(img_g4),                    \
                      static_cast<const uint4*>(img_g8),                                                         \
                      static_cast<const uint4*>(a.img_unshift), a.out, classes)
-  static const uint32_t classes = [] {
-    const char* e = std::getenv("ANNETY_CRC_SORTED_CLASSES");
-    return e ? (uint32_t)std::atoi(e) & 31u : kSortedClassesDefault;
-  }();
-  static const int nt = [] {
-    const char* e = std::getenv("ANNETY_CRC_SORTED_NT");
-    return e && e[0] >= '0' && e[0] <= '7' ? e[0] - '0' : kSortedNtDefault;
-  }();
-  switch (nt) {
-#define ANNETY_SORTED_CASE(NT)                  \
-  case NT:                                      \
-    if (a.update) ANNETY_SORTED_LAUNCH(true, NT); \
-    else ANNETY_SORTED_LAUNCH(false, NT);       \
-    break;
-    ANNETY_SORTED_CASE(0)
-    ANNETY_SORTED_CASE(1)
-    ANNETY_SORTED_CASE(2)
-    ANNETY_SORTED_CASE(3)
-    ANNETY_SORTED_CASE(4)
-    ANNETY_SORTED_CASE(5)
-    ANNETY_SORTED_CASE(6)
-    ANNETY_SORTED_CASE(7)
-#undef ANNETY_SORTED_CASE
-    default: break;
-  }
+  constexpr uint32_t classes = kSortedClassesDefault;
+  if (a.update) ANNETY_SORTED_LAUNCH(true, kSortedNtDefault);
+  else ANNETY_SORTED_LAUNCH(false, kSortedNtDefault);
 #undef ANNETY_SORTED_LAUNCH
   return hipGetLastError();
 }

@@ -141,23 +141,5 @@ constexpr uint32_t kLdsQuarterOff = kLdsStitchUnshiftOff + kLdsUnshiftBytes;
 constexpr uint32_t kLdsMidOff = kLdsQuarterOff + 512;
 constexpr uint32_t kMidMaps = 6;  // P(2..7); P(1) = G(8) of the segment set, P(0) = identity
 constexpr uint32_t kLdsStitchImageBytes = kLdsMidOff + kMidMaps * 512;  // 163840: all of the CU's LDS
-// Line-stream variable path (crc32_stream.hip). Device image "stream" (offsets relative to its start); the
-// line-stream kernel stages [0, kStreamPartBytes) behind the common part:
-//   [0, 8 KiB)              U_lo set: shift_{-m}, m = 0..15, (k, m, v) at (k*16 + m)*64 + v*4
-//   [8 KiB, +4 KiB)         U_hi set: shift_{-16h}, h = 0..7, (k, h, v) at (k*8 + h)*64 + v*4
-//   [12 KiB, +512 B)        init terms I[a] = shift_{128-a}(0xFFFFFFFF), a = 0..127: crc32_long's init seen from
-//                           the end of the line whose byte a starts the payload
-//   [12.5 KiB, +3 KiB)      scan maps P(i) = shift_{2^i * 128}, i = 0..5, each (k, v) at k*64 + v*4 (uniform)
-//   [15.5 KiB, +4 KiB)      (global only) power matrices M(i) = shift_{2^i * 128}, i = 0..31, 32 columns each:
-//                           the cross-chunk join, read with scalar loads
-constexpr uint32_t kStreamULoOff = 0;
-constexpr uint32_t kStreamUHiOff = 8192;
-constexpr uint32_t kStreamInitOff = 12288;
-constexpr uint32_t kStreamPowOff = 12800;
-constexpr uint32_t kStreamPartBytes = kStreamPowOff + 6 * 512;  // 15872
-constexpr uint32_t kStreamMatOff = kStreamPartBytes;
-constexpr uint32_t kStreamImgBytes = kStreamMatOff + 32 * 32 * 4;  // 19968
-constexpr uint32_t kLdsStreamOff = kLdsCommonBytes;
-constexpr uint32_t kLdsStreamImageBytes = kLdsStreamOff + kStreamPartBytes;  // 147456
 
 }  // namespace annety_crc

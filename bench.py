@@ -64,11 +64,10 @@ def parse():
     p.add_argument("--strong", action="store_true",
                    help="fixed configs: --payloads (default 1M) is the TOTAL over all ranks, split into contiguous "
                         "shards (strong scaling); default is per GPU (weak scaling)")
-    p.add_argument("--var-path", choices=["arena", "auto", "sorted", "stream"], default="arena",
+    p.add_argument("--var-path", choices=["arena", "auto", "sorted"], default="arena",
                    help="config 3: arena = one pass over the packed arena + per-payload stitch (annety_crc32_batch_var_arena); "
                         "auto = annety_crc32_batch_var, which picks the arena path itself from the batch's recorded extent; "
-                        "sorted = the length-bucketed path only (ANNETY_CRC_VAR_PATH=sorted); stream = the line-stream "
-                        "path (ANNETY_CRC_VAR_PATH=stream)")
+                        "sorted = the length-bucketed path only (ANNETY_CRC_VAR_PATH=sorted)")
     p.add_argument("--chunks", type=int, default=None,
                    help="N>1: chunks per shard for the pipelined gather (default 1 for config 1: step s's gather "
                         "overlaps step s+1's kernel; 2 for config 4, one-rank rehearsal 1/2/4 chunks "
@@ -222,8 +221,7 @@ class Workload:
             self.var_path = args.var_path
             self.desc = (f"BASELINE config 3: {self.n} payloads, Zipf(1.1) lengths 64 B-64 KiB packed unaligned, "
                          f"{total / 2**30:.3f} GiB per GPU, " + {"arena": "arena path", "auto": "automatic path choice",
-                                                                  "sorted": "sorted path",
-                                                                  "stream": "line-stream path"}[args.var_path])
+                                                                  "sorted": "sorted path"}[args.var_path])
         # strong scaling: shards differ by at most one payload; the digest buffer is padded (zeros) to the
         # largest so that every rank's gather moves the same count
         self.n_pad = -(-self.n_total // world) if getattr(args, "strong", False) else self.n
@@ -346,18 +344,29 @@ def cpu_baseline(h: np.ndarray, offs: np.ndarray, lens: np.ndarray, budget_s: fl
                 return reps * nbytes / dt / 2 ** 30, reps
 
     st_rate, st_reps = rate(1, budget_s * 0.3)
-    mt_rate, mt_reps = rate(threads, budget_s * 0.7)
+    mt_rate, mt_reps = rate(threads, budget_s * 0.6)
+    # the reference at hardware_concurrency() threads, what annety's one-loop-per-thread
+    # pool (src/EventLoopPool.cc:55-66) would use on this host; the job's scheduler share may cap what these
+    # threads get (affinity_cpus says how many CPUs the process may run on)
+    all_rate, all_reps = rate(host_cpus, budget_s * 0.1) if host_cpus > threads else (mt_rate, mt_reps)
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = None
     return {
         "value": round(mt_rate, 3),
         "unit": "GiB/s",
         "cores": threads,
         "host_cpus": host_cpus,
+        "all_cores_value": round(all_rate, 3),
+        "all_cores": host_cpus,
+        "affinity_cpus": affinity,
         "kind": kind,
         "compile_flags": REF_FLAGS if kind == "reference" else "gcc -O2 (oracle/Makefile, C restatement)",
         "single_thread_value": round(st_rate, 3),
         "sample": f"{n} payloads / {nbytes / 2**20:.1f} MiB prefix of the GPU workload copied to host (memory-resident, "
                   f"far above the host caches), crc32_long per payload, payload-parallel over {threads} threads x "
-                  f"{mt_reps} passes (+ 1 thread x {st_reps})",
+                  f"{mt_reps} passes (+ 1 thread x {st_reps}; + {host_cpus} threads x {all_reps} for all_cores_value)",
     }
 
 
@@ -464,7 +473,7 @@ def main():
         raise SystemExit("--strong applies to the fixed 1 KiB configs (1, 4)")
     if args.chunks is None:
         args.chunks = 2 if args.config == 4 else 1
-    if args.var_path in ("sorted", "stream", "auto"):
+    if args.var_path in ("sorted", "auto"):
         os.environ["ANNETY_CRC_VAR_PATH"] = args.var_path  # read once by the library: before it loads
     if multi and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < args.hw_queues:
         # HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default); the compute stream, torch's

@@ -92,10 +92,9 @@ int annety_crc_stream_release(void* stream);
  * slot between streams so far, device-wide synchronisations so far (0 outside annety_crc_shutdown). */
 int annety_crc_scratch_stats(int device, uint64_t* slots, uint64_t* handoffs, uint64_t* device_syncs);
 /* The path annety_crc32_batch_var / annety_crc32_update_batch_var take, process-wide (initial value from
- * ANNETY_CRC_VAR_PATH = auto | sorted | stream; ANNETY_CRC_VAR_AUTO=0 means sorted): 0 = automatic arena or
- * length-sorted choice from recorded extents (below), 1 = the length-sorted path, 2 = the line stream (every
- * payload's 128-byte lines in one stream walked in equal chunks, crc32_stream.hip). Digests do not depend on
- * it. get returns the current mode. */
+ * ANNETY_CRC_VAR_PATH = auto | sorted; ANNETY_CRC_VAR_AUTO=0 means sorted): 0 = automatic arena or
+ * length-sorted choice from recorded extents (below), 1 = the length-sorted path. Any other mode returns
+ * ANNETY_CRC_EINVAL. Digests do not depend on it. get returns the current mode. */
 int annety_crc_set_var_path(int mode);
 int annety_crc_get_var_path(void);
 /* Calls of annety_crc32_batch_var / annety_crc32_update_batch_var on `device` (n >= 1024) that took the

@@ -273,6 +273,25 @@ def test_product_kernels_do_not_spill(tmp_path):
     assert not spilling, spilling
 
 
+OPERATIONAL_KNOBS = {"ANNETY_CRC_SYNC_STAGES", "ANNETY_CRC_STREAM_SLOTS", "ANNETY_CRC_VAR_PATH", "ANNETY_CRC_VAR_AUTO",
+                     "ANNETY_CRC_SPLIT", "ANNETY_CRC_SEG", "ANNETY_CRC_FRAMES_PACK", "ANNETY_CRC_PACK_THREADS",
+                     "ANNETY_CRC_WALK_THREADS"}
+
+
+def test_product_library_reads_only_operational_knobs():
+    """The shipping libannety_crc.so names no A/B or probe switch (ANNETY_CRC_SORTED_CLASSES and
+    ANNETY_CRC_STREAM_PROBE made the product write wrong digests): every ANNETY_CRC_* string in the binary is an
+    operational knob (scratch slots, variable-path choice, split policy, staging/walk threads, stage syncs),
+    none of which changes a digest. The A/B switches exist only in -DANNETY_CRC_AB builds (crc32_kernels.h)."""
+    blob = open(_lib.lib_path(), "rb").read()
+    names = {m.decode() for m in re.findall(rb"ANNETY_CRC_[A-Z0-9_]+", blob)}
+    assert names, "no environment knob found at all: the string scan is broken"
+    assert names <= OPERATIONAL_KNOBS, sorted(names - OPERATIONAL_KNOBS)
+    for probe in ("SORTED_CLASSES", "STREAM_PROBE", "STITCH_MID", "STITCH_PIPE", "SORTED_NT", "LINES_NT", "FIXED_NT",
+                  "SORTED_FUSED"):
+        assert ("ANNETY_CRC_" + probe).encode() not in blob, probe
+
+
 def test_verify_host_iov_arguments_without_device():
     """annety_lhc_verify_host_iov argument rules (before any device work): bad length type, a NULL buffer
     with a size, missing outputs; an all-empty call walks nothing and needs no device."""

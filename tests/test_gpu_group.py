@@ -3,8 +3,9 @@ GPU box's one device: the sharded device-resident batch with the chunked digest 
 and the host batch staged over the group's PCIe links - bit-exact against the oracle. A one-device
 group builds the communicator but sends nothing (the root computes into its output directly): the
 grouped ncclSend/ncclRecv branch of crc32_group.cpp runs only with two or more devices, which this
-one-GPU box cannot provide, and stays unverified on hardware. Its transfer schedule is the host-only
-annety_crc_group_schedule, checked for 8 devices on the CPU (tests/test_capi.py)."""
+one-GPU box cannot provide; test_group_all_visible_devices runs it whenever the box shows two or more
+devices (the driver's 8-GPU node). Its transfer schedule is the host-only annety_crc_group_schedule, checked
+for 8 devices on the CPU (tests/test_capi.py)."""
 import numpy as np
 import pytest
 
@@ -32,6 +33,37 @@ def test_group_device_shards(gpu):
         out = g.batch_fixed([torch.from_numpy(host[: n2 * 1003]).to(gpu)], L2, stride=1003, chunks=4)
         torch.cuda.synchronize()
         assert np.array_equal(out.cpu().numpy().view(np.uint32), oracle.batch_fixed(host, n2, L2, 1003))
+
+
+def test_group_all_visible_devices(gpu):
+    """Every visible device in one group (crc32_group.cpp: ncclCommInitAll, per-device compute streams,
+    grouped ncclSend/ncclRecv of each chunk's digests to the root while the next chunk computes), 1M x 1 KiB
+    per device as in BASELINE config 4's shards, every digest against the oracle. Skips on a one-GPU box: the
+    send/recv branch needs a second device (missing item 4)."""
+    import torch
+
+    from annety_amd import sharded
+
+    ndev = torch.cuda.device_count()
+    if ndev < 2:
+        pytest.skip("one visible device: the group's RCCL send/recv branch needs two or more")
+    n, L = 1 << 20, 1024
+    shards, want = [], []
+    for d in range(ndev):
+        g = torch.Generator(device=torch.device("cuda", d))
+        g.manual_seed(9100 + d)
+        s = torch.randint(0, 256, (n * L,), dtype=torch.uint8, device=torch.device("cuda", d), generator=g)
+        shards.append(s)
+        want.append(oracle.batch_fixed_mt(s.cpu().numpy(), n, L, threads=16))
+    with sharded.DeviceGroup(list(range(ndev))) as grp:
+        for chunks in (1, 4):
+            out = grp.batch_fixed(shards, L, chunks=chunks)
+            torch.cuda.synchronize(0)
+            got = out.cpu().numpy().view(np.uint32)
+            assert got.size == n * ndev
+            for d in range(ndev):
+                bad = np.nonzero(got[d * n:(d + 1) * n] != want[d])[0]
+                assert bad.size == 0, (chunks, d, bad.size, bad[:4].tolist())
 
 
 def test_group_host_batch(gpu):

@@ -1,14 +1,13 @@
-"""The line-stream variable path (crc32_stream.hip: scan + stream + cross-chunk fixup) against the oracle.
+"""The length-sorted variable path (annety_crc_set_var_path("sorted"): counting sort by line count, then the
+length classes) on every layout and edge case, against the oracle.
 
-Every batch runs through annety_crc32_batch_var / annety_crc32_update_batch_var with the path set to "stream"
-(annety_crc_set_var_path). Small batches already exercise the chunk machinery hard: the stream launch cuts the
-positions into one chunk per wave (2048 waves on 256 CUs), so a batch of a few thousand lines has a chunk
-boundary every 64 lines and most payloads cross one; a single long payload crosses hundreds (the fixup's
-per-lane pieces and its loop over 64-piece groups). Edge cases after the reference's own (empty payloads,
-lengths 1-3 at line ends, payloads of exactly one line, the init's four bytes spilling into the next line),
-layouts from the fuzz families (packed, gapped, shuffled, overlapping, repeated), update registers, repeated
-calls of changing sizes on one stream (the scan's alternating status sets) and on several streams, and the
-full BASELINE config-3 batch."""
+Every batch runs through annety_crc32_batch_var / annety_crc32_update_batch_var with the path forced to
+"sorted", so batches of any size take it (the automatic entry would move dense batches to the arena path).
+Edge cases after the reference's own (empty payloads, lengths 1-3 at line ends, payloads of exactly one line,
+the init's four bytes spilling into the next line), layouts from the fuzz families (packed, gapped, shuffled,
+overlapping, repeated), long payloads among short ones, update registers, and repeated calls of changing sizes
+on one stream (the counting sort's alternating cursor sets) and on several streams. (Round 4 ran these against
+the line-stream path, which was removed in round 5: it never beat the sorted path)"""
 import numpy as np
 import pytest
 
@@ -18,10 +17,10 @@ pytestmark = pytest.mark.gpu
 
 
 @pytest.fixture
-def stream_path(gpu):
+def sorted_path(gpu):
     import annety_amd
 
-    prev = annety_amd.set_var_path("stream")
+    prev = annety_amd.set_var_path("sorted")
     yield gpu
     annety_amd.set_var_path(prev)
 
@@ -41,7 +40,7 @@ def _run(dev, host, offs, lens, states=None, out=None):
     else:
         res = annety_amd.crc32_batch_var(d, o, ln, out=out)
     torch.cuda.synchronize()
-    assert annety_amd.last_kernels().startswith("crc32_stream_scan_kernel"), annety_amd.last_kernels()
+    assert annety_amd.last_kernels().startswith("crc32_extent_kernel<count>"), annety_amd.last_kernels()
     return res.cpu().numpy().view(np.uint32)
 
 
@@ -53,13 +52,13 @@ def _check(dev, host, offs, lens, ctx="", states=None):
     assert bad.size == 0, (ctx, bad.size, bad[:8].tolist(), np.asarray(lens)[bad[:8]].tolist())
 
 
-def test_golden_fixtures(stream_path, golden):
+def test_golden_fixtures(sorted_path, golden):
     """The compiled reference's recorded digests: every length 0..300 and a sweep to 64 KiB at 12 start
     alignments, and the Zipf batch; then packed batches of 1..1000 payloads against the oracle."""
     import annety_amd
     import torch
 
-    dev = stream_path
+    dev = sorted_path
     g = golden("lengths.json")
     arena = torch.from_numpy(oracle.lcg_bytes(g["arena_bytes"], g["seed"])).to(dev)
     lens = torch.tensor(g["lengths"], dtype=torch.int32, device=dev)
@@ -82,7 +81,7 @@ def test_golden_fixtures(stream_path, golden):
         _check(dev, host, offs, lens, ctx=n)
 
 
-def test_every_short_length_at_every_line_offset(stream_path):
+def test_every_short_length_at_every_line_offset(sorted_path):
     # lengths 0..300 starting at every offset of a 128-byte line (the init spill, 1-3 byte payloads at line
     # ends, exactly-one-line payloads), each as its own payload in one batch over one buffer
     rng = np.random.default_rng(12)
@@ -92,37 +91,37 @@ def test_every_short_length_at_every_line_offset(stream_path):
         for a in (0, 1, 60, 64, 124, 125, 126, 127):
             lens.append(L)
             offs.append(1024 + 128 * ((L * 7 + a) % 300) + a)
-    _check(stream_path, host, offs, lens, ctx="short")
-    _check(stream_path, host, offs, lens, ctx="short-upd",
+    _check(sorted_path, host, offs, lens, ctx="short")
+    _check(sorted_path, host, offs, lens, ctx="short-upd",
            states=rng.integers(0, 2 ** 32, len(lens), dtype=np.uint64).astype(np.uint32))
 
 
-def test_empty_and_all_empty(stream_path):
+def test_empty_and_all_empty(sorted_path):
     rng = np.random.default_rng(13)
     host = rng.integers(0, 256, 4096, dtype=np.uint8)
-    _check(stream_path, host, [0, 5, 9], [0, 0, 0], ctx="all empty")
+    _check(sorted_path, host, [0, 5, 9], [0, 0, 0], ctx="all empty")
     lens = np.array([0, 3, 0, 0, 200, 0, 1, 0])
-    _check(stream_path, host, np.arange(8) * 300, lens, ctx="some empty")
+    _check(sorted_path, host, np.arange(8) * 300, lens, ctx="some empty")
     st = rng.integers(0, 2 ** 32, 8, dtype=np.uint64).astype(np.uint32)
-    _check(stream_path, host, np.arange(8) * 300, lens, ctx="some empty upd", states=st)
+    _check(sorted_path, host, np.arange(8) * 300, lens, ctx="some empty upd", states=st)
 
 
-def test_long_payloads_across_many_chunks(stream_path):
-    # one payload of 1 MiB (8192 lines: with a chunk per 64 lines it crosses 127 boundaries, two rounds of
-    # the fixup's 64 lanes), then long payloads among short ones
+def test_long_payloads_among_short(sorted_path):
+    # single payloads of 1 and 3 MiB (one lane group walks thousands of rounds), then long payloads among
+    # short ones (every length class in one launch)
     rng = np.random.default_rng(14)
     host = rng.integers(0, 256, (3 << 20) + 777, dtype=np.uint8)
-    _check(stream_path, host, [3], [1 << 20], ctx="1 MiB")
-    _check(stream_path, host, [77], [(3 << 20) - 100], ctx="3 MiB")
+    _check(sorted_path, host, [3], [1 << 20], ctx="1 MiB")
+    _check(sorted_path, host, [77], [(3 << 20) - 100], ctx="3 MiB")
     lens = rng.integers(0, 100, 2000)
     lens[::97] = rng.integers(100_000, 400_000, lens[::97].size)
     offs = rng.integers(0, host.size - lens + 1)
-    _check(stream_path, host, offs, lens, ctx="mixed")
+    _check(sorted_path, host, offs, lens, ctx="mixed")
     st = rng.integers(0, 2 ** 32, lens.size, dtype=np.uint64).astype(np.uint32)
-    _check(stream_path, host, offs, lens, ctx="mixed upd", states=st)
+    _check(sorted_path, host, offs, lens, ctx="mixed upd", states=st)
 
 
-def test_fuzz_layouts(stream_path):
+def test_fuzz_layouts(sorted_path):
     from test_gpu_fuzz import _layout, _lengths
 
     rng = np.random.default_rng(20261017)
@@ -137,63 +136,31 @@ def test_fuzz_layouts(stream_path):
             offs = (offs * cap / need * 0.5).astype(np.int64)
         host = rng.integers(0, 256, cap, dtype=np.uint8)
         states = rng.integers(0, 2 ** 32, n, dtype=np.uint64).astype(np.uint32) if fam % 3 == 2 else None
-        _check(stream_path, host, offs, lens, ctx=(fam, kind, n), states=states)
+        _check(sorted_path, host, offs, lens, ctx=(fam, kind, n), states=states)
 
 
-def test_repeated_calls_changing_sizes_and_streams(stream_path):
-    # the scan's status sets alternate per call on a stream's slot and each call zeroes the records the
-    # previous one left: sizes that grow and shrink (more and fewer tiles than the call before), then the
-    # same on four streams in turn
+def test_repeated_calls_changing_sizes_and_streams(sorted_path):
+    # the counting sort's two cursor sets alternate per call on a stream's slot and each call zeroes the set
+    # of the next: sizes that grow and shrink, then the same on four streams in turn
     import torch
 
     import annety_amd
 
     rng = np.random.default_rng(15)
     host = rng.integers(0, 256, 4 << 20, dtype=np.uint8)
-    d = torch.from_numpy(host).to(stream_path)
-    streams = [torch.cuda.Stream(device=stream_path) for _ in range(4)]
+    d = torch.from_numpy(host).to(sorted_path)
+    streams = [torch.cuda.Stream(device=sorted_path) for _ in range(4)]
     for rep, n in enumerate([5000, 100, 9000, 9000, 1, 20000, 2048, 2049, 4096, 300]):
         lens = rng.integers(0, 400, n)
         offs = rng.integers(0, host.size - 400, n)
         want = oracle.batch_var_mt(host, offs.astype(np.uint64), lens.astype(np.uint32), threads=8)
         for s in [None] + (streams if rep % 3 == 0 else []):
             with torch.cuda.stream(s) if s is not None else torch.cuda.stream(torch.cuda.current_stream()):
-                o = torch.from_numpy(offs).to(stream_path)
-                ln = torch.from_numpy(lens.astype(np.int32)).to(stream_path)
+                o = torch.from_numpy(offs).to(sorted_path)
+                ln = torch.from_numpy(lens.astype(np.int32)).to(sorted_path)
                 out = annety_amd.crc32_batch_var(d, o, ln)
             torch.cuda.synchronize()
             got = out.cpu().numpy().view(np.uint32)
             assert np.array_equal(got, want), (rep, n, int((got != want).sum()))
     for s in streams:
         annety_amd.stream_release(s)
-
-
-def test_config3_full_stream(stream_path):
-    import torch
-
-    import annety_amd
-    from test_gpu_fullsize import THREADS, _bench
-
-    gpu = stream_path
-    lens, offs = _bench().zipf_batch(0x5EED)
-    total = int(lens.sum())
-    g = torch.Generator(device=gpu)
-    g.manual_seed(4242)
-    data = torch.randint(0, 256, (total,), dtype=torch.uint8, device=gpu, generator=g)
-    d_off = torch.from_numpy(offs).to(gpu)
-    d_len = torch.from_numpy(lens.astype(np.int32)).to(gpu)
-    got = annety_amd.crc32_batch_var(data, d_off, d_len)
-    torch.cuda.synchronize()
-    print("config 3 (stream): digests done", flush=True)
-    host = data.cpu().numpy()
-    want = oracle.batch_var_mt(host, offs, lens, THREADS)
-    bad = np.nonzero(got.cpu().numpy().view(np.uint32) != want)[0]
-    assert bad.size == 0, f"{bad.size} digest mismatches, first {bad[:8]} (lengths {lens[bad[:8]]})"
-    rng = np.random.default_rng(5)
-    states = rng.integers(0, 2 ** 32, lens.size, dtype=np.uint64).astype(np.uint32)
-    d_state = torch.from_numpy(states.view(np.int32).copy()).to(gpu)
-    annety_amd.crc32_update_batch_var(d_state, data, d_off, d_len)
-    torch.cuda.synchronize()
-    want = oracle.batch_var_mt(host, offs, lens, THREADS, states=states)
-    bad = np.nonzero(d_state.cpu().numpy().view(np.uint32) != want)[0]
-    assert bad.size == 0, f"{bad.size} register mismatches, first {bad[:8]}"
