@@ -42,12 +42,19 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(f) <= t for f in _inputs())
 
 
-def build(force: bool = False, verbose: bool = False) -> str:
-    if not force and up_to_date():
+AB_LIB = os.path.join(ROOT, "microbench", "libannety_crc_ab.so")
+
+
+def build(force: bool = False, verbose: bool = False, ab: bool = False) -> str:
+    """The product library, or with ab=True the design-space build (-DANNETY_CRC_AB: the A/B and probe switches
+    read from the environment, crc32_kernels.h) at microbench/libannety_crc_ab.so, loaded with ANNETY_CRC_LIB.
+    The A/B build is never the product: tests and the bench load LIB."""
+    lib = AB_LIB if ab else LIB
+    if not force and not ab and up_to_date():
         return LIB
-    tmp = os.path.join(PKG, "build")
+    tmp = os.path.join(PKG, "build", "ab" if ab else "")
     os.makedirs(tmp, exist_ok=True)
-    common = ["-std=c++17", "-O3", "-fPIC", f"-I{INCLUDE}", f"-I{CSRC}", "-Wall"]
+    common = ["-std=c++17", "-O3", "-fPIC", f"-I{INCLUDE}", f"-I{CSRC}", "-Wall"] + (["-DANNETY_CRC_AB"] if ab else [])
     cmds, objs = [], []
     for s in SOURCES:
         src = os.path.join(CSRC, s)
@@ -63,7 +70,7 @@ def build(force: bool = False, verbose: bool = False) -> str:
     with concurrent.futures.ThreadPoolExecutor(max_workers=min(len(cmds), 8)) as ex:
         for f in [ex.submit(subprocess.run, c, check=True) for c in cmds]:
             f.result()
-    out_tmp = LIB + ".tmp"
+    out_tmp = lib + ".tmp"
     # RCCL for the device-group entry points (crc32_group.cpp); rpath so the library loads without
     # LD_LIBRARY_PATH on any box with this ROCm image
     cmd = [hipcc(), f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", out_tmp] + objs + [
@@ -71,9 +78,11 @@ def build(force: bool = False, verbose: bool = False) -> str:
     if verbose:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
-    os.replace(out_tmp, LIB)
-    return LIB
+    os.replace(out_tmp, lib)
+    return lib
 
 
 if __name__ == "__main__":
-    print(build(force=True, verbose=True))
+    import sys
+
+    print(build(force=True, verbose=True, ab="--ab" in sys.argv))

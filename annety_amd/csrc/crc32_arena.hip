@@ -69,9 +69,6 @@ __device__ __forceinline__ uint32_t seg_map(uint32_t t, uint32_t idx, const uint
   return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6] ^ r[7]);
 }
 
-__device__ __forceinline__ uint32_t gload4(uint64_t addr) {
-  return *(const __attribute__((address_space(1))) uint32_t*)addr;
-}
 
 // Two 64-byte windows from register 0, four 32-byte chains: raw(window) = shift_32(raw(first half)) ^
 // raw(second half).
@@ -617,10 +614,9 @@ __global__ __launch_bounds__(kBucketThreads) void crc32_bucket_place(const uint6
   basep[t] = start + mine;
   if (blockIdx.x == 0) {
     bk.cursor_next[t] = 0u;
-    // classes by line count (bucket = 1023 - lines): >= 128 lines, 24..127, < 24, run at G = 32 / 16 / 4
-    // (crc32_capi.cpp run_var_sorted_in; on the config-3 batch the middle and small classes ran 12 % and
-    // 15 % faster at G = 16 / 4 than at 8 / 2: profiles/r02/ab4_stages.log)
-    constexpr uint32_t b16 = kBucketCount - 128, b4 = kBucketCount - 24;
+    // classes by line count (bucket = 1023 - lines): >= 9 lines (crc32_kernels.hip var_class_w8), an empty
+    // middle range, <= 8 lines (var_class<4>)
+    constexpr uint32_t b16 = kBucketCount - 9, b4 = kBucketCount - 9;  // bucket 1015 = 8 lines
     if (t == 0) bk.ranges[0] = 0u;
     if (t == b16) bk.ranges[1] = bk.ranges[2] = start;
     if (t == b4) bk.ranges[3] = bk.ranges[4] = start;

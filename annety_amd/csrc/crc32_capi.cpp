@@ -83,6 +83,7 @@ struct HostImages {
   std::vector<uint32_t> unshift; // 24 maps x 128 words (U_lo[0..15], U_hi[0..7])
   std::vector<uint32_t> sb;      // arena superblock join: (k, v, g) = shift_{(7-g)*1024}(v << 4k); byte map
   std::vector<uint32_t> stitch;  // arena stitch: segment maps F/G/UL/UB, unshift, shift_32 (crc32_math.h)
+  std::vector<uint32_t> w8;      // sorted path, >= 9-line class: join, byte maps, unshift (crc32_math.h kLdsW8*)
 };
 
 // Apply matrix m to (v << 4k) for every nibble value: the 16-entry table of one nibble position.
@@ -210,6 +211,24 @@ const HostImages& host_images() {
       for (uint32_t c = 2; c < 2 + kMidMaps; c++) nibble_tables(shift_matrix((uint64_t)8192 * c), mid.data() + (c - 2) * 128);
       put_set(m + (kLdsMidOff - kLdsMapOff) / 4, mid.data(), kMidMaps);
     }
+    img.w8.assign(kW8ImgBytes / 4, 0);
+    {
+      uint32_t* m = img.w8.data();
+      for (uint32_t jj = 0; jj < 8; jj++) {  // (k, v, j) at (k*16 + v)*8 + j words
+        uint32_t nt[8 * 16];
+        nibble_tables(shift_matrix((uint64_t)(7 - jj) * kChunkBytes), nt);
+        for (int kk = 0; kk < 8; kk++)
+          for (int v = 0; v < 16; v++) m[(kk * 16 + v) * 8 + jj] = nt[kk * 16 + v];
+      }
+      const uint64_t shifts[2] = {64, 7 * kChunkBytes};  // byte tables: half-line join, round advance
+      for (int m_i = 0; m_i < 2; m_i++) {
+        const Gf2Mat sm = shift_matrix(shifts[m_i]);
+        uint32_t* bm = m + (kLdsW8HalfOff - kLdsCommonBytes + m_i * 4096) / 4;
+        for (uint32_t kk = 0; kk < 4; kk++)
+          for (uint32_t e = 0; e < 256; e++) bm[kk * 256 + e] = gf2_apply(sm, e << (8 * kk));
+      }
+      std::memcpy(m + (kLdsW8UnshiftOff - kLdsCommonBytes) / 4, img.unshift.data(), img.unshift.size() * 4);
+    }
   });
   return img;
 }
@@ -304,6 +323,7 @@ struct DeviceCtx {
   uint32_t* d_unshift = nullptr;
   void* d_sb = nullptr;
   void* d_stitch = nullptr;
+  void* d_w8 = nullptr;
   void* d_zero = nullptr;  // 256 zero bytes
   Staging stg;
   std::mutex stg_mu;  // one host-staged batch at a time per device
@@ -328,12 +348,12 @@ size_t grid_cus(const DeviceCtx& c) { return (size_t)std::max(1, c.cus - g_reser
 std::mutex g_init_mu;
 
 void free_images(DeviceCtx& c) {
-  void* bufs[] = {c.d_slice, c.d_groups, c.d_unshift, c.d_sb, c.d_stitch, c.d_zero};
+  void* bufs[] = {c.d_slice, c.d_groups, c.d_unshift, c.d_sb, c.d_stitch, c.d_w8, c.d_zero};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   c.d_slice = c.d_groups = nullptr;
   c.d_unshift = nullptr;
-  c.d_sb = c.d_stitch = c.d_zero = nullptr;
+  c.d_sb = c.d_stitch = c.d_w8 = c.d_zero = nullptr;
 }
 
 int init_device_locked(int dev) {
@@ -357,6 +377,8 @@ int init_device_locked(int dev) {
     if ((e = hipMalloc(&c.d_unshift, img.unshift.size() * 4)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMalloc(&c.d_sb, img.sb.size() * 4)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMalloc(&c.d_stitch, img.stitch.size() * 4)) != hipSuccess) { rc = hip_fail(e); break; }
+    if ((e = hipMalloc(&c.d_w8, img.w8.size() * 4)) != hipSuccess) { rc = hip_fail(e); break; }
+    if ((e = hipMemcpy(c.d_w8, img.w8.data(), img.w8.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMalloc(&c.d_zero, 256)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMemset(c.d_zero, 0, 256)) != hipSuccess) { rc = hip_fail(e); break; }
     if ((e = hipMemcpy(c.d_sb, img.sb.data(), img.sb.size() * 4, hipMemcpyHostToDevice)) != hipSuccess) { rc = hip_fail(e); break; }
@@ -555,7 +577,7 @@ int run_var_sorted_in(DeviceCtx& c, ScratchSlot* slot, const void* d_base, size_
   }
   slot->data.sorts++;
   int rc = ANNETY_CRC_OK;
-  if (sorted_fused()) {  // the three length classes in one launch (crc32_var_sorted_kernel)
+  if (sorted_fused()) {  // the length classes in one launch (crc32_var_sorted_kernel)
     VarLaunch a{};
     a.update = update;
     a.base = d_base;
@@ -566,10 +588,10 @@ int run_var_sorted_in(DeviceCtx& c, ScratchSlot* slot, const void* d_base, size_
     a.img_unshift = c.d_unshift;
     a.out = d_out;
     a.max_blocks = grid_cus(c);
-    const hipError_t e = launch_var_sorted(a, group_image(c, 32), group_image(c, 16), group_image(c, 4), group_image(c, 8), stream);
+    const hipError_t e = launch_var_sorted(a, c.d_w8, group_image(c, 8), stream);
     return e == hipSuccess ? ANNETY_CRC_OK : hip_fail(e);
   }
-  const uint32_t groups[3] = {32, 16, 4};  // lanes per payload of the long / middle / small class
+  const uint32_t groups[3] = {32, 16, 4};  // (A/B builds) lanes per payload of the >= 9-line / empty / small class
   for (int k = 0; k < 3 && rc == ANNETY_CRC_OK; k++)
     rc = run_var(c, d_base, n, 0, 0, groups[k], bk.desc, bk.ranges + 2 * k, d_out, stream, update);
   return rc;
@@ -1246,16 +1268,10 @@ static int encode_batch(const FrameRules& r, const void* d_src, const uint64_t* 
   int rc = stream_ctx(static_cast<hipStream_t>(stream), &c);
   if (rc) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  uint32_t* dig = nullptr;
-  HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&dig), n * sizeof(uint32_t), s));
-  rc = annety_crc32_batch_var(d_src, d_src_off, d_len, n, dig, stream);
-  if (rc == ANNETY_CRC_OK) {
-    hipError_t e = launch_lhc_encode(d_src, d_src_off, d_len, n, r.T, r.enc_min, r.enc_max, d_dst, d_frame_off, dig, s);
-    if (e != hipSuccess) rc = hip_fail(e);
-  }
-  hipError_t e = hipFreeAsync(dig, s);
-  if (rc == ANNETY_CRC_OK && e != hipSuccess) rc = hip_fail(e);
-  return rc;
+  // one pass: each payload read once, its frame (header, copy, CRC trailer) written once (crc32_frames.hip)
+  HIP_TRY(launch_lhc_encode_fused(d_src, d_src_off, d_len, n, r.T, r.enc_min, r.enc_max, d_dst, d_frame_off, c->d_zero,
+                                  c->d_slice, group_image(*c, 8), c->d_unshift, grid_cus(*c), s));
+  return ANNETY_CRC_OK;
 }
 
 int annety_lhc_encode_batch(const void* d_src, const uint64_t* d_src_off, const uint32_t* d_len, size_t n,

@@ -220,6 +220,18 @@ __device__ __forceinline__ uint4 gload16(uint64_t addr) {
   const v4u32 x = *p;
   return make_uint4(x.x, x.y, x.z, x.w);
 }
+__device__ __forceinline__ uint32_t gload4(uint64_t addr) {
+  return *(const __attribute__((address_space(1))) uint32_t*)addr;
+}
+__device__ __forceinline__ uint32_t gload1(uint64_t addr) {
+  return *(const __attribute__((address_space(1))) uint8_t*)addr;
+}
+// Global (not flat) stores: a flat store would also count in lgkmcnt, and every LDS wait of the fold
+// (word4x2's s_waitcnt lgkmcnt(0)) would then wait for it.
+__device__ __forceinline__ void gstore4(uint64_t addr, uint32_t v) { *(__attribute__((address_space(1))) uint32_t*)addr = v; }
+__device__ __forceinline__ void gstore1(uint64_t addr, uint32_t v) {
+  *(__attribute__((address_space(1))) uint8_t*)addr = (uint8_t)v;
+}
 
 // The streaming loops raise their wave priority while they issue the next task's loads, so the
 // other wave on the SIMD (in its fold) does not delay them: config-1 kernel -0.5..1.0 %, arena line

@@ -63,10 +63,10 @@ struct VarLaunch {
 };
 
 hipError_t launch_var(const VarLaunch& a, hipStream_t stream);
-// The sorted path's three length classes (G = 32 / 16 / 4, a.range = their 6 bounds) in one launch;
-// a.group and a.img_group are ignored.
-hipError_t launch_var_sorted(const VarLaunch& a, const void* img_g32, const void* img_g16, const void* img_g4,
-                             const void* img_g8, hipStream_t stream);
+// The sorted path's length classes in one launch (a.range = their 6 bounds: >= 9 lines, empty, <= 8 lines);
+// img_w8 = the w8 image (kW8ImgBytes, crc32_math.h), img_g8 = the G = 8 group part; a.group and a.img_group are
+// ignored.
+hipError_t launch_var_sorted(const VarLaunch& a, const void* img_w8, const void* img_g8, hipStream_t stream);
 
 // Long payloads cut into end-aligned segments (crc32_kernels.hip): descriptors for the variable kernel,
 // then the combine fold with powers[(m-1)*32 + bit] = shift_{m*seg}(1 << bit), m = 1..S-1.
@@ -210,9 +210,12 @@ hipError_t launch_arena_lines(const ArenaLaunch& a, hipStream_t stream);
 // LengthHeaderCodec frames (crc32_frames.hip)
 hipError_t launch_lhc_compare(const void* stream_base, const uint64_t* off, const uint32_t* len, size_t n,
                               const uint32_t* digest, uint8_t* ok, hipStream_t stream);
-hipError_t launch_lhc_encode(const void* src, const uint64_t* src_off, const uint32_t* len, size_t n, int T,
-                             int64_t enc_min, int64_t enc_max, void* dst, const uint64_t* dst_off,
-                             const uint32_t* digest, hipStream_t stream);
+// One pass per frame: CRC, header, payload copy and trailer (crc32_frames.hip lhc_encode_fused_kernel). zero_line:
+// 128 zero bytes (device); img_g8 = the G = 8 group part of the var image.
+hipError_t launch_lhc_encode_fused(const void* src, const uint64_t* src_off, const uint32_t* len, size_t n, int T,
+                                   int64_t enc_min, int64_t enc_max, void* dst, const uint64_t* dst_off,
+                                   const void* zero_line, const void* img_slice, const void* img_g8,
+                                   const void* img_unshift, size_t max_blocks, hipStream_t stream);
 int fixed_kernel_block();
 // Records, for annety_crc_last_kernels, that the current entry point enqueued `name` (crc32_capi.cpp).
 void note_kernel(const char* name);

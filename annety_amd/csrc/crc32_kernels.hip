@@ -431,8 +431,9 @@ __device__ __forceinline__ uint4 raw_task(size_t t, size_t end, const uint8_t* b
 //   PROBE (microbench only; product = 0): bit 0 drops the byte masks, bit 1 the unshift - wrong
 //        digests, used to measure what those stages cost (microbench/ab3.hip).
 //   STAGE: which parts of the LDS image this call stages - 2 = all of it, and none when the block has no
-//        task (a kernel of its own); 1 = all of it always; 0 = only the G-specific group part (the later
-//        length classes of crc32_var_sorted_kernel, whose first class staged the rest).
+//        task (a kernel of its own); 1 = all of it always; 0 = only the G-specific group part; 3 = the group part
+//        and the inverse-shift tables (the later classes of crc32_var_sorted_kernel, whose first class staged
+//        the common part).
 template <int G, bool SORTED, bool UPD, int VWG, int PROBE, int STAGE>
 __device__ __forceinline__ void var_class(uint4* lds4, const uint8_t* __restrict__ base, size_t n, uint64_t fstride,
                                           uint32_t flen, const uint4* __restrict__ desc,
@@ -489,6 +490,8 @@ __device__ __forceinline__ void var_class(uint4* lds4, const uint8_t* __restrict
   load(dec0, r0, A);
   if constexpr (STAGE == 0)
     load_image<kLdsImageBytes, kBlock, kLdsImageBytes, kLdsCommonBytes>(lds4, img_slice, img_group);
+  else if constexpr (STAGE == 3)
+    load_image<kLdsVarImageBytes, kBlock, kLdsImageBytes, kLdsCommonBytes>(lds4, img_slice, img_group, img_unshift);
   else
     load_image<kLdsVarImageBytes>(lds4, img_slice, img_group, img_unshift);
   __syncthreads();
@@ -603,377 +606,7 @@ __device__ __forceinline__ void var_class(uint4* lds4, const uint8_t* __restrict
   }
 }
 
-// Byte masks of one half-line (bytes [64 h, 64 h + 64) of a payload line, h = the lane's l3), for the line with
-// real index li (var_class's masks, per half): li < 0 = virtual (zero), li = 0 the first line (bytes before the
-// payload dropped, the init or the caller's register on payload bytes 0..3), li = 1 the spill line when the
-// first holds fewer than 4 payload bytes, li = nlines - 1 the last (bytes after the payload dropped).
-//   keep bits [A8, H8) of the line; non-UPD: complement bits [A8, B8) (the init); UPD: xor the register at S8.
-struct HalfMask {
-  int32_t A8, B8, H8, S8;
-  uint32_t reg;
-  uint32_t need;  // some byte of the line changes
-};
-template <bool UPD>
-__device__ __forceinline__ HalfMask half_mask(int32_t li, const VarTask& cur) {
-  HalfMask m;
-  const bool first = li == 0;
-  const bool spill = li == 1 && cur.lead > 124 && cur.len >= 4;
-  m.A8 = li < 0 ? 1024 : (first ? (int32_t)cur.lead * 8 : 0);
-  m.H8 = li == (int32_t)cur.nlines - 1 ? (int32_t)cur.tailend * 8 : 1024;
-  m.S8 = first || spill ? ((int32_t)cur.lead - (first ? 0 : 128)) * 8 : 4096;  // register byte 0 (UPD)
-  m.reg = cur.len < 4 ? 0u : cur.state;
-  m.B8 = first || spill ? (cur.len < 4 ? m.A8 : ((int32_t)cur.lead + 4 - (first ? 0 : 128)) * 8) : m.A8;
-  m.need = (li < 2 || li >= (int32_t)cur.nlines - 1) ? 1u : 0u;
-  return m;
-}
-template <bool UPD, int O>
-__device__ __forceinline__ void apply_half_mask(uint4 (&v)[8], const HalfMask& m, uint32_t h) {
-  const int32_t base8 = (int32_t)h * 512;  // bit offset of the half in its line
-#pragma unroll
-  for (int i = 0; i < 4; i++) {
-    uint32_t* w = reinterpret_cast<uint32_t*>(&v[O + i]);
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const int32_t p8 = base8 + (i * 16 + q * 4) * 8;
-      const uint32_t keepA = (uint32_t)(0xFFFFFFFFull << clamp032(m.A8 - p8));
-      const uint32_t keepH = (uint32_t)(0xFFFFFFFFull >> clamp032(p8 + 32 - m.H8));
-      if constexpr (UPD) {
-        const int32_t x = m.S8 - p8;
-        const uint32_t sw = x >= 32 || x <= -32 ? 0u : (x >= 0 ? m.reg << x : m.reg >> -x);
-        w[q] = (keepA & keepH & w[q]) ^ sw;
-      } else {
-        const uint32_t keepB = (uint32_t)(0xFFFFFFFFull << clamp032(m.B8 - p8));
-        w[q] = keepA & keepH & (w[q] ^ ~keepB);
-      }
-    }
-  }
-}
-template <bool UPD, int O>
-__device__ __forceinline__ void mask_half(uint4 (&v)[8], int32_t li, const VarTask& cur, uint32_t h) {
-  apply_half_mask<UPD, O>(v, half_mask<UPD>(li, cur), h);
-}
-[[maybe_unused]] __device__ __forceinline__ int32_t lane_xor8(int32_t x) { return __builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, false); }
-
-// The G = 32 and G = 16 length classes with coalesced nontemporal loads (crc32_fixed32_nt_kernel's access
-// shape on the sorted descriptors). A wave holds NG = 64 / G lane groups, each stepping through its own
-// (payload, round) sequence exactly like var_class<G>; per step a group's round is G consecutive absolute lines,
-// read as 1 KiB pieces: load i covers piece 2 (i >> 2) + (i & 1) of group (i >> 1) & 1 (G = 32) or piece i >> 2
-// of group i & 3 (G = 16), with the groups' line bases broadcast from their first lanes. A lane's line index is
-// clamped to its payload's lines (virtual lines of the first round re-read the first line and are masked to
-// zero; a group without a task reads one line of the buffer). After transpose_blocks lane l holds half l3 of
-// lines jA and jA + G/2 of its group's round (jA = 8 l4 + (l & 7) for G = 32, l & 7 for G = 16); both halves
-// are masked where they hold a payload edge, the round register enters the first halves, and the half join
-// leaves lane l the register of line jl = jA + (G/2) l3 (nibble-table half join: the var image has no byte
-// tables). STAGE as var_class (1: the whole image, also for a block without work; 0: the group part only).
-template <int G, bool UPD, int STAGE>
-__device__ __forceinline__ void var_class_nt(uint4* lds4, const uint8_t* __restrict__ base,
-                                             const uint4* __restrict__ desc, const uint32_t* __restrict__ range,
-                                             const uint4* __restrict__ img_slice, const uint4* __restrict__ img_group,
-                                             const uint4* __restrict__ img_unshift, uint32_t* __restrict__ out) {
-  static_assert(G == 16 || G == 32, "two or four lane groups per wave");
-  constexpr int NG = 64 / G;
-  const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
-  const uint32_t l = threadIdx.x & 63, l3 = (l >> 3) & 1, l4 = (l >> 4) & 1;
-  const size_t gid = group_id<kBlock, G, kVwg>();
-  const size_t ngroups = ((size_t)gridDim.x * kBlock) / G;
-  const size_t t_begin = range[0], t_end = range[1];
-  LaneCtx k;
-  k.L0 = (threadIdx.x & 31) << 3;
-  k.L1 = k.L0 | (1u << 16);
-  const uint32_t jA = (G == 32 ? 8 * l4 : 0u) + (l & 7);  // line of v[0..3]; v[4..7] holds line jA + G/2
-  const uint32_t jl = jA + (G / 2) * l3;
-  k.slot4 = jl << 2;
-  const uint32_t chunk = 16u * (4u * l3 + 2u * ((l >> 5) & 1u) + l4);  // coalesced_lane_offset without the line
-  const uint64_t b0 = (uint64_t)(uintptr_t)base;
-  const uint64_t safe_line = b0 >> 7;
-
-  auto raw = [&](size_t t) { return raw_task<true>(t, t_end, base, desc, 0, 0); };
-  auto load = [&](const VarTask& tk, uint32_t r, uint4 (&v)[8]) {
-    const int32_t rel0 = (int32_t)(r * G) - (int32_t)tk.vlead;
-    const int32_t rmax = tk.valid ? (int32_t)tk.nlines - 1 : 0;
-    const uint64_t ln0 = tk.valid ? tk.line0 : safe_line;
-    const uint32_t lo = (uint32_t)ln0, hi = (uint32_t)(ln0 >> 32);
-    int32_t rel_g[NG], max_g[NG];
-    uint64_t ln_g[NG];
-#pragma unroll
-    for (int g = 0; g < NG; g++) {
-      rel_g[g] = __builtin_amdgcn_readlane(rel0, g * G);
-      max_g[g] = __builtin_amdgcn_readlane(rmax, g * G);
-      ln_g[g] = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, g * G) << 32) |
-                (uint32_t)__builtin_amdgcn_readlane((int)lo, g * G);
-    }
-    // branch-free (a scalar branch between two load sequences made the compiler drain the loads at the merge:
-    // 284 us against 222 per config-3 call): per group a scalar base at its payload's first line, per lane a
-    // 32-bit offset of its clamped line
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      const int g = G == 32 ? (i >> 1) & 1 : i & 3;
-      const int piece = G == 32 ? 2 * (i >> 2) + (i & 1) : i >> 2;
-      const int32_t rel = min(max(rel_g[g] + 8 * piece + (int32_t)(l & 7), 0), max_g[g]);
-      const uint8_t* gb = base + ((ln_g[g] << 7) - b0);
-      const v4u32 x = __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(gb + ((uint32_t)rel * 128u + chunk)));
-      v[i] = make_uint4(x.x, x.y, x.z, x.w);
-    }
-  };
-
-  size_t t0 = t_begin + gid;
-  if (!__syncthreads_or(t0 < t_end)) {  // the block has no task of this class
-    if constexpr (STAGE == 1) {  // (the next classes stage only their group part)
-      load_image<kLdsVarImageBytes>(lds4, img_slice, img_group, img_unshift);
-      __syncthreads();
-    }
-    return;
-  }
-  VarTask dec0 = decode_task<G>(raw(t0), t0 < t_end);
-  if constexpr (UPD) dec0.state = dec0.valid ? out[dec0.p] : 0u;
-  uint32_t r0 = 0;
-  size_t t1 = dec0.rounds > 1 ? t0 : t0 + ngroups;
-  uint32_t r1 = dec0.rounds > 1 ? 1u : 0u;
-  uint4 d1 = raw(t1);
-
-  uint4 A[8], B[8];
-  load(dec0, r0, A);
-  if constexpr (STAGE == 0)
-    load_image<kLdsImageBytes, kBlock, kLdsImageBytes, kLdsCommonBytes>(lds4, img_slice, img_group);
-  else
-    load_image<kLdsVarImageBytes>(lds4, img_slice, img_group, img_unshift);
-  __syncthreads();
-
-  uint32_t s = 0;
-  auto compute = [&](uint4 (&v)[8], const VarTask& cur, uint32_t r_c) {
-    transpose_blocks(v);
-    const int32_t liA = (int32_t)(r_c * G + jA) - (int32_t)cur.vlead;
-    const int32_t liB = liA + G / 2;
-    const int32_t last = (int32_t)cur.nlines - 1;
-    // virtual lines of a first round: zeroed by selects (cheap); the payload's first, spill and last lines:
-    // the byte masks, on the one half-branch that holds them (a first round with both halves' general masks
-    // cost twice the VALU of the whole fold)
-    if (liA < 0 || liB < 0) {
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        v[i] = liA < 0 ? make_uint4(0u, 0u, 0u, 0u) : v[i];
-        v[4 + i] = liB < 0 ? make_uint4(0u, 0u, 0u, 0u) : v[4 + i];
-      }
-    }
-    const bool spill = cur.lead > 124 && cur.len >= 4;
-    if (liA == 0 || (liA == 1 && spill) || liA == last) mask_half<UPD, 0>(v, liA, cur, l3);
-    if (liB == 0 || (liB == 1 && spill) || liB == last) mask_half<UPD, 4>(v, liB, cur, l3);
-    // the round register (shift_{(G-1)*128} of the lane's register, 0 at a payload's first round) enters the
-    // first half of its line: lanes with l3 = 0 fold the first halves of their own line and of lane ^ 8's
-    const uint32_t sin = nibble_map_uniform(s, lds, kLdsRoundOff);
-    const uint32_t sp = (uint32_t)__builtin_amdgcn_mov_dpp((int)sin, 0x128, 0xF, 0xF, false);  // lane ^ 8's
-    v[0].x ^= l3 ? 0u : sin;
-    v[4].x ^= l3 ? 0u : sp;
-    {
-      uint32_t xa = v[0].x, xb = v[4].x;
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        word4x2(xa, v[i].y, xb, v[4 + i].y, k);
-        word4x2(xa, v[i].z, xb, v[4 + i].z, k);
-        word4x2(xa, v[i].w, xb, v[4 + i].w, k);
-        word4x2(xa, i + 1 < 4 ? v[i + 1].x : 0u, xb, i + 1 < 4 ? v[5 + i].x : 0u, k);
-      }
-      const uint32_t send = l3 ? xa : xb;
-      const uint32_t got = (uint32_t)__builtin_amdgcn_mov_dpp((int)send, 0x128, 0xF, 0xF, false);
-      const uint32_t first = l3 ? got : xa, second = l3 ? xb : got;
-      s = nibble_map_uniform(first, lds, kLdsHalfOff) ^ second;  // shift_64
-    }
-    if (r_c == cur.rounds - 1) {
-      uint32_t t = group_xor_reduce<G>(nibble_map_lane(s, lds, k.slot4));
-      if (cur.valid && (l & (G - 1)) == G - 1) {
-        const uint32_t over = 128 - cur.tailend;  // trailing zero bytes of the last line
-        if (over) {
-          t = nibble_map_uniform(t, lds, kLdsUnshiftOff + (over & 15u) * 512);
-          t = nibble_map_uniform(t, lds, kLdsUnshiftOff + 8192 + (over >> 4) * 512);
-        }
-        if constexpr (UPD) {
-          if (cur.len < 4) t ^= shift_bits(cur.state, 8u * cur.len);
-          out[cur.p] = t;
-        } else {
-          if (cur.len < 4) {
-            constexpr uint32_t k1 = shift_bits(kInit, 8), k2 = shift_bits(kInit, 16), k3 = shift_bits(kInit, 24);
-            t ^= cur.len == 1 ? k1 : (cur.len == 2 ? k2 : k3);
-          }
-          out[cur.p] = ~t;
-        }
-      }
-      s = 0;
-    }
-  };
-
-  auto step = [&](uint4 (&cur_buf)[8], uint4 (&nxt_buf)[8]) {
-    // every group of the wave still in its task (r1 > 0): its descriptor is decoded already (no load in the
-    // branch, so the loads in flight are not drained at the merge; update mode decodes every step, since it
-    // loads the register there)
-    VarTask dec1 = dec0;
-    if (UPD || __builtin_amdgcn_ballot_w64(r1 == 0) != 0) {
-      dec1 = decode_task<G>(d1, t1 < t_end);
-      if constexpr (UPD) dec1.state = dec1.valid ? out[dec1.p] : 0u;
-    }
-    const bool more = r1 + 1 < dec1.rounds;
-    const size_t t2 = more ? t1 : t1 + ngroups;
-    const uint32_t r2 = more ? r1 + 1 : 0u;
-    const uint4 d2 = raw(t2);
-    ANNETY_PRIO_HI();
-    load(dec1, r1, nxt_buf);
-    __builtin_amdgcn_sched_barrier(0);
-    ANNETY_PRIO_LO();
-    compute(cur_buf, dec0, r0);
-    dec0 = dec1;
-    r0 = r1;
-    t1 = t2;
-    r1 = r2;
-    d1 = d2;
-  };
-
-  // wave-uniform loop: the loads and the cross-lane steps need every group (a finished group reads one
-  // line of the buffer and stores nothing)
-  while (__builtin_amdgcn_ballot_w64(dec0.valid) != 0) {
-    step(A, B);
-    step(B, A);
-  }
-}
-
-// The small class (< 24 lines) with coalesced nontemporal loads, at G = 8: a wave's eight lane groups (lanes
-// 8m..8m+7) each step through their own (payload, round) sequence, a round being 8 consecutive absolute lines =
-// 1 KiB = exactly one load. Load i reads the round of lane group m(i) = (i >> 2) + 2 (i & 1) + 4 ((i >> 1) & 1)
-// (its line base broadcast from lane 8 m(i)), so that after transpose_blocks and the half join lane l holds
-// line l & 7 of its own group's round (crc32_onekib_nt_kernel's layout). Before the join a lane holds half l3 of
-// line l & 7 of two groups: its own and lane ^ 8's; the masks of the partner's line come over DPP.
-template <bool UPD>
-__device__ __forceinline__ void var_class_nt8(uint4* lds4, const uint8_t* __restrict__ base,
-                                              const uint4* __restrict__ desc, const uint32_t* __restrict__ range,
-                                              const uint4* __restrict__ img_slice, const uint4* __restrict__ img_group,
-                                              uint32_t* __restrict__ out) {
-  constexpr int G = 8;
-  const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
-  const uint32_t l = threadIdx.x & 63, l3 = (l >> 3) & 1, j = l & 7;
-  const size_t gid = group_id<kBlock, G, kVwg>();
-  const size_t ngroups = ((size_t)gridDim.x * kBlock) / G;
-  const size_t t_begin = range[0], t_end = range[1];
-  LaneCtx k;
-  k.L0 = (threadIdx.x & 31) << 3;
-  k.L1 = k.L0 | (1u << 16);
-  k.slot4 = (threadIdx.x & 31) << 2;  // join slot: j = slot & 7
-  const uint32_t lane_off = coalesced_lane_offset(l);
-  const uint64_t b0 = (uint64_t)(uintptr_t)base;
-  const uint64_t safe_line = b0 >> 7;
-
-  auto raw = [&](size_t t) { return raw_task<true>(t, t_end, base, desc, 0, 0); };
-  auto load = [&](const VarTask& tk, uint32_t r, uint4 (&v)[8]) {
-    const int32_t rel0 = (int32_t)(r * G) - (int32_t)tk.vlead;
-    const int32_t rmax = tk.valid ? (int32_t)tk.nlines - 1 : 0;
-    const uint64_t ln0 = tk.valid ? tk.line0 : safe_line;
-    const uint32_t lo = (uint32_t)ln0, hi = (uint32_t)(ln0 >> 32);
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-      const int src = 8 * ((i >> 2) + 2 * (i & 1) + 4 * ((i >> 1) & 1));
-      const int32_t rel_g = __builtin_amdgcn_readlane(rel0, src), max_g = __builtin_amdgcn_readlane(rmax, src);
-      const uint64_t ln_g = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, src) << 32) |
-                            (uint32_t)__builtin_amdgcn_readlane((int)lo, src);
-      const int32_t rel = min(max(rel_g + (int32_t)j, 0), max_g);
-      const uint64_t off = ((ln_g + (uint64_t)rel) << 7) + (lane_off & 127u) - b0;
-      const v4u32 x = __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(base + off));
-      v[i] = make_uint4(x.x, x.y, x.z, x.w);
-    }
-  };
-
-  size_t t0 = t_begin + gid;
-  if (!__syncthreads_or(t0 < t_end)) return;
-  VarTask dec0 = decode_task<G>(raw(t0), t0 < t_end);
-  if constexpr (UPD) dec0.state = dec0.valid ? out[dec0.p] : 0u;
-  uint32_t r0 = 0;
-  size_t t1 = dec0.rounds > 1 ? t0 : t0 + ngroups;
-  uint32_t r1 = dec0.rounds > 1 ? 1u : 0u;
-  uint4 d1 = raw(t1);
-
-  uint4 A[8], B[8];
-  load(dec0, r0, A);
-  load_image<kLdsImageBytes, kBlock, kLdsImageBytes, kLdsCommonBytes>(lds4, img_slice, img_group);
-  __syncthreads();
-
-  uint32_t s = 0;
-  auto compute = [&](uint4 (&v)[8], const VarTask& cur, uint32_t r_c) {
-    transpose_blocks(v);
-    const int32_t li = (int32_t)(r_c * G + j) - (int32_t)cur.vlead;
-    const HalfMask mo = half_mask<UPD>(li, cur);
-    HalfMask mp;  // lane ^ 8's line (same position j in the partner group)
-    mp.A8 = lane_xor8(mo.A8);
-    mp.H8 = lane_xor8(mo.H8);
-    if constexpr (UPD) {
-      mp.S8 = lane_xor8(mo.S8);
-      mp.reg = (uint32_t)lane_xor8((int32_t)mo.reg);
-    } else {
-      mp.B8 = lane_xor8(mo.B8);
-    }
-    mp.need = (uint32_t)lane_xor8((int32_t)mo.need);
-    // v[0..3]: half l3 of the line of lane l & ~8's group, v[4..7]: of lane l | 8's
-    if (l3 ? mp.need : mo.need) apply_half_mask<UPD, 0>(v, l3 ? mp : mo, l3);
-    if (l3 ? mo.need : mp.need) apply_half_mask<UPD, 4>(v, l3 ? mo : mp, l3);
-    const uint32_t sin = nibble_map_uniform(s, lds, kLdsRoundOff);  // shift_{7*128}; 0 at a first round
-    const uint32_t sp = (uint32_t)lane_xor8((int32_t)sin);
-    v[0].x ^= l3 ? 0u : sin;
-    v[4].x ^= l3 ? 0u : sp;
-    {
-      uint32_t xa = v[0].x, xb = v[4].x;
-#pragma unroll
-      for (int i = 0; i < 4; i++) {
-        word4x2(xa, v[i].y, xb, v[4 + i].y, k);
-        word4x2(xa, v[i].z, xb, v[4 + i].z, k);
-        word4x2(xa, v[i].w, xb, v[4 + i].w, k);
-        word4x2(xa, i + 1 < 4 ? v[i + 1].x : 0u, xb, i + 1 < 4 ? v[5 + i].x : 0u, k);
-      }
-      const uint32_t send = l3 ? xa : xb;
-      const uint32_t got = (uint32_t)lane_xor8((int32_t)send);
-      const uint32_t first = l3 ? got : xa, second = l3 ? xb : got;
-      s = nibble_map_uniform(first, lds, kLdsHalfOff) ^ second;  // shift_64
-    }
-    if (r_c == cur.rounds - 1) {
-      uint32_t t = group_xor_reduce<G>(nibble_map_lane(s, lds, k.slot4));
-      if (cur.valid && j == G - 1) {
-        const uint32_t over = 128 - cur.tailend;
-        if (over) {
-          t = nibble_map_uniform(t, lds, kLdsUnshiftOff + (over & 15u) * 512);
-          t = nibble_map_uniform(t, lds, kLdsUnshiftOff + 8192 + (over >> 4) * 512);
-        }
-        if constexpr (UPD) {
-          if (cur.len < 4) t ^= shift_bits(cur.state, 8u * cur.len);
-          out[cur.p] = t;
-        } else {
-          if (cur.len < 4) {
-            constexpr uint32_t k1 = shift_bits(kInit, 8), k2 = shift_bits(kInit, 16), k3 = shift_bits(kInit, 24);
-            t ^= cur.len == 1 ? k1 : (cur.len == 2 ? k2 : k3);
-          }
-          out[cur.p] = ~t;
-        }
-      }
-      s = 0;
-    }
-  };
-
-  auto step = [&](uint4 (&cur_buf)[8], uint4 (&nxt_buf)[8]) {
-    VarTask dec1 = decode_task<G>(d1, t1 < t_end);
-    if constexpr (UPD) dec1.state = dec1.valid ? out[dec1.p] : 0u;
-    const bool more = r1 + 1 < dec1.rounds;
-    const size_t t2 = more ? t1 : t1 + ngroups;
-    const uint32_t r2 = more ? r1 + 1 : 0u;
-    const uint4 d2 = raw(t2);
-    ANNETY_PRIO_HI();
-    load(dec1, r1, nxt_buf);
-    __builtin_amdgcn_sched_barrier(0);
-    ANNETY_PRIO_LO();
-    compute(cur_buf, dec0, r0);
-    dec0 = dec1;
-    r0 = r1;
-    t1 = t2;
-    r1 = r2;
-    d1 = d2;
-  };
-  while (__builtin_amdgcn_ballot_w64(dec0.valid) != 0) {
-    step(A, B);
-    step(B, A);
-  }
-}
+__device__ __forceinline__ int32_t lane_xor8(int32_t x) { return __builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, false); }
 
 template <int G, bool SORTED, bool UPD = false, int VWG = kVwg, int PROBE = 0>
 __global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __restrict__ base, size_t n,
@@ -989,76 +622,375 @@ __global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __rest
                                            img_unshift, out);
 }
 
-// The sorted path's three length classes in one launch (ranges[0..5] = the classes' [begin, end) in desc,
-// longest first): each block runs its share of the G = 32 class, then of the G = 16 class (restaging only
-// the group part of the image), then of the G = 4 class. A block that finishes a class early starts the
-// next one instead of waiting for the class's slowest lane groups (three launches drained each class:
-// a 64 KiB-payload launch loses ~24 us to its tail), and two launch gaps go.
-//   NT (bits, ANNETY_CRC_SORTED_NT, default 3): 1 = the G = 32 class with coalesced nontemporal loads
-//   (var_class_nt), 2 = the G = 16 class too, 4 = the small class at G = 8 (var_class_nt8); unset classes load
-//   per line (small: G = 4). Config 3, one class alone (profiles/r04/sorted_nt/classes.log): G = 32 150.4 us
-//   coalesced / 182.6 per line, G = 16 68.6 / 63.8, small 53.2 (G = 8) / 40.9 (G = 4); fused, masks 1 and 3 the
-//   same, 7 slower.
-template <bool UPD, int NT>
+// ---------------------------------------------------------------------------------------------
+// The length-sorted path's class of payloads of >= 9 lines (round 5): lane groups of G = 8 on
+// coalesced nontemporal 1 KiB loads, with the steady-state round of crc32_onekib_nt_kernel and no per-lane
+// masks, clamps or address arithmetic in it.
+//
+// A payload of nl lines (absolute 128-byte lines L0..L1) is cut into R = (nl - h) / 8 + 1 rounds:
+//   round 0 ("head"): lines [0, 8) read start-aligned, of which the first h = ((nl - 1) mod 8) + 1 are the
+//            payload's (bytes before the payload start masked, lines >= h zeroed), then each lane's register is
+//            moved (8 - h) lanes up inside its group (ds_bpermute), so that the group holds the head end-aligned,
+//            and the init (or the caller's register) enters as the register shift_{128-lead}(init) of line 0;
+//   rounds 1 .. R-1 ("body"): the 1 KiB pieces [h + 8 (r - 1), h + 8 r): whole lines, except that the last
+//            round's line 7 is the payload's last line (bytes after the payload end masked, removed after the
+//            join by the inverse shift of the line's overhang).
+// A group's rounds are read from one scalar base per round (the group's round address broadcast from its first
+// lane), so a body round costs the loads, the transpose, the round register and the fold, as in config 1.
+// The wave's 8 groups take 8 consecutive tasks of the length-sorted list (equal line counts in the same
+// bucket), so they start and finish together: every step in which no group is in its head or last round (or
+// idle) takes the unmasked branch, wave-uniformly; the rest (about 2 per 8 payloads, 15 % of config 3's steps)
+// take the masked one. Groups still step through their own task sequences (t += number of groups), so unequal
+// lengths never idle a group.
+struct W8Task {
+  uint64_t a0;  // address of the payload's first line (128-aligned)
+  uint32_t lead, te, h, R, p, state;
+  bool valid;
+};
+__device__ __forceinline__ W8Task decode_w8(uint4 d, bool valid) {
+  W8Task k;
+  const uint64_t a = ((uint64_t)d.y << 32) | d.x;
+  const uint64_t e = a + d.z;  // length >= 9 lines' worth, so > 0
+  const uint64_t L0 = a >> 7;
+  const uint32_t nl = (uint32_t)(((e - 1) >> 7) - L0 + 1);
+  k.a0 = L0 << 7;
+  k.lead = (uint32_t)(a & 127);
+  k.te = (uint32_t)(((e - 1) & 127) + 1);
+  k.h = ((nl - 1) & 7u) + 1;
+  k.R = ((nl - k.h) >> 3) + 1;
+  k.p = d.w;
+  k.state = 0;
+  k.valid = valid;
+  return k;
+}
+// shift_{-m}, m in [0, 128): U_hi[m >> 4] o U_lo[m & 15] from the w8 image
+__device__ __forceinline__ uint32_t w8_unshift(uint32_t t, uint32_t m, const uint32_t* lds) {
+  t = nibble_map_uniform(t, lds, kLdsW8UnshiftOff + (m & 15u) * 512);
+  return nibble_map_uniform(t, lds, kLdsW8UnshiftOff + 8192 + (m >> 4) * 512);
+}
+// shift_{(7-j)*128} from the unreplicated join tables
+__device__ __forceinline__ uint32_t w8_join(uint32_t s, const uint32_t* lds, uint32_t j) {
+  const uint32_t* t = lds + kLdsW8JoinOff / 4 + j;
+  uint32_t r[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) r[k] = t[k * 128 + __builtin_amdgcn_ubfe(s, 4 * k, 4) * 8];
+  return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6] ^ r[7]);
+}
+
+//   STAGE: 1 = stage the whole image (also for a block without work of this class), 0 = only the w8 part (the
+//   common part is in place).
+//   PROBE (A/B builds only, microbench/sorted_probe.py; product = 0): bit 0 = every step takes the unmasked
+//   branch, bit 1 = no fold (the data are xored into the register) - wrong digests, used to measure what the
+//   masked rounds and the fold cost.
+template <bool UPD, int STAGE, int PROBE = 0>
+__device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restrict__ base,
+                                             const uint4* __restrict__ desc, const uint32_t* __restrict__ range,
+                                             const uint4* __restrict__ img_slice, const uint4* __restrict__ img_w8,
+                                             uint32_t* __restrict__ out) {
+  constexpr int G = 8;
+  const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
+  const uint32_t l = threadIdx.x & 63, l3 = (l >> 3) & 1, j = l & 7;
+  const size_t gid = group_id<kBlock, G, kVwg>();
+  const size_t ngroups = ((size_t)gridDim.x * kBlock) / G;
+  const size_t t_begin = range[0], t_end = range[1];
+  LaneCtx k;
+  k.L0 = (threadIdx.x & 31) << 3;
+  k.L1 = k.L0 | (1u << 16);
+  k.slot4 = 0;  // (the w8 join is unreplicated)
+  const uint32_t voff = coalesced_lane_offset(l);  // line j, chunk 4 l3 + 2 l5 + l4 of a group's 1 KiB round
+  const uint64_t b0 = (uint64_t)(uintptr_t)base;
+  auto raw = [&](size_t t) { return raw_task<true>(t, t_end, base, desc, 0, 0); };
+  // Load i reads the round of lane group m(i) = (i >> 2) + 2 (i & 1) + 4 ((i >> 1) & 1), so that after
+  // transpose_blocks lane l holds half l3 of line j of the even group of its pair (l >> 3 & ~1) in v[0..3] and of
+  // the odd one in v[4..7] (crc32_onekib_nt_kernel's layout). Invalid groups decode the last task of the class
+  // (raw_task clamps), so every address is inside a payload of >= 9 lines.
+  auto load = [&](const W8Task& tk, uint32_t r, uint4 (&v)[8]) __attribute__((always_inline)) {
+    const uint64_t ad = tk.a0 + (r == 0 ? 0ull : (uint64_t)tk.h * 128u + (uint64_t)(r - 1) * 1024u);
+    const uint32_t lo = (uint32_t)ad, hi = (uint32_t)(ad >> 32);
+#pragma unroll
+    for (int i = 0; i < 8; i++) {
+      const int src = 8 * ((i >> 2) + 2 * (i & 1) + 4 * ((i >> 1) & 1));
+      const uint64_t g = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, src) << 32) |
+                         (uint32_t)__builtin_amdgcn_readlane((int)lo, src);
+      const uint8_t* gb = base + (g - b0);
+      const v4u32 x = __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(gb + voff));
+      v[i] = make_uint4(x.x, x.y, x.z, x.w);
+    }
+  };
+
+  size_t t0 = t_begin + gid;
+  if (!__syncthreads_or(t0 < t_end)) {  // the block has no task of this class
+    if constexpr (STAGE == 1) {
+      load_image<kLdsW8ImageBytes, kBlock, kLdsCommonBytes>(lds4, img_slice, nullptr, img_w8);
+      __syncthreads();
+    }
+    return;
+  }
+  // Pipeline: the load side holds the task whose round rL it loads this step (dL, index tL) and the raw
+  // descriptor of the task after it (rn), fetched every step from the same address while dL runs: when dL
+  // ends, rn was first requested a whole task earlier and the decode never waits on HBM (fetching only the
+  // next step's descriptor, as var_class does, exposed a miss at every task switch: 205 us for the loads
+  // and the bookkeeping alone on config 3). The compute side (dC, rC) is the load side one step later.
+  W8Task dL = decode_w8(raw(t0), t0 < t_end);
+  if constexpr (UPD) dL.state = dL.valid ? out[dL.p] : 0u;
+  size_t tL = t0;
+  uint4 rn = raw(tL + ngroups);
+
+  uint4 A[8], B[8];
+  load(dL, 0, A);
+  W8Task dC = dL;
+  uint32_t rC = 0, rL = 1;
+  if constexpr (STAGE == 0)
+    load_image<kLdsW8ImageBytes, kBlock, kLdsCommonBytes, kLdsCommonBytes>(lds4, img_slice, nullptr, img_w8);
+  else
+    load_image<kLdsW8ImageBytes, kBlock, kLdsCommonBytes>(lds4, img_slice, nullptr, img_w8);
+  __syncthreads();
+
+  uint32_t s = 0;
+  auto fold = [&](uint4 (&v)[8]) __attribute__((always_inline)) {
+    // the round register (shift_{7*128} of the lane's register; 0 after a payload's last round) enters the
+    // first halves: lanes with l3 = 0 fold the first half of their own line and of lane ^ 8's
+    const uint32_t sin = byte_map64(s, lds, kLdsW8RoundOff);
+    const uint32_t sp = (uint32_t)__builtin_amdgcn_mov_dpp((int)sin, 0x128, 0xF, 0xF, false);  // lane ^ 8's
+    v[0].x ^= l3 ? 0u : sin;
+    v[4].x ^= l3 ? 0u : sp;
+    s = fold_halves(v, k, lds, l3, kLdsW8HalfOff);
+  };
+  auto compute = [&](uint4 (&v)[8], const W8Task& cur, uint32_t r_c) __attribute__((always_inline)) {
+    transpose_blocks(v);
+    const bool body = cur.valid && r_c > 0 && r_c + 1 < cur.R;
+    if constexpr ((PROBE & 2) != 0) {
+      uint32_t x = s;
+#pragma unroll
+      for (int i = 0; i < 8; i++) x ^= v[i].x ^ v[i].y ^ v[i].z ^ v[i].w;
+      s = x;
+      if (cur.valid && r_c + 1 == cur.R && j == 7) out[cur.p] = s;
+      return;
+    }
+    if ((PROBE & 1) != 0 || __builtin_amdgcn_ballot_w64(!body) == 0) {  // every group in a body round: no masks
+      fold(v);
+      if constexpr ((PROBE & 1) != 0) {
+        if (cur.valid && r_c + 1 == cur.R && j == 7) out[cur.p] = s;
+      }
+      return;
+    }
+    // Masked round. This lane's group (l >> 3): keep bytes [lo, hi) of half q of its line j, for q = l3 (own use)
+    // and 1 - l3 (sent to lane ^ 8, whose v holds this group's half 1 - l3 ... = the partner's own half).
+    const bool head = cur.valid && r_c == 0, last = cur.valid && r_c + 1 == cur.R;
+    const int32_t line_lo = head && j == 0 ? (int32_t)cur.lead : 0;
+    const int32_t line_hi = !cur.valid || (head && j >= cur.h) ? 0 : (last && j == 7 ? (int32_t)cur.te : 128);
+    const int32_t lo_own = min(max(line_lo - 64 * (int32_t)l3, 0), 64), hi_own = min(max(line_hi - 64 * (int32_t)l3, 0), 64);
+    const int32_t lo_oth = min(max(line_lo - 64 * (int32_t)(l3 ^ 1), 0), 64),
+                  hi_oth = min(max(line_hi - 64 * (int32_t)(l3 ^ 1), 0), 64);
+    // lane ^ 8 holds the other group of the pair and computed its bounds for our half as its "other" half
+    const int32_t lo_par = lane_xor8(lo_oth), hi_par = lane_xor8(hi_oth);
+    // v[0..3]: the even group of the pair (own if l3 = 0), v[4..7]: the odd one
+    const int32_t lo_a = l3 ? lo_par : lo_own, hi_a = l3 ? hi_par : hi_own;
+    const int32_t lo_b = l3 ? lo_own : lo_par, hi_b = l3 ? hi_own : hi_par;
+    if (__builtin_amdgcn_ballot_w64(lo_a > 0 || hi_a < 64 || lo_b > 0 || hi_b < 64) != 0) {
+      uint4 va[4] = {v[0], v[1], v[2], v[3]}, vb[4] = {v[4], v[5], v[6], v[7]};
+      mask_line<4>(va, lo_a * 8, hi_a * 8);
+      mask_line<4>(vb, lo_b * 8, hi_b * 8);
+#pragma unroll
+      for (int i = 0; i < 4; i++) {
+        v[i] = va[i];
+        v[4 + i] = vb[i];
+      }
+    }
+    fold(v);
+    // head round: move the registers (8 - h) lanes up inside the group (lines [0, h) become the round's last h
+    // lines), then line 0's register gains the init as a register at the payload start, shift_{128-lead}(init)
+    if (__builtin_amdgcn_ballot_w64(head) != 0) {
+      const uint32_t up = 8 - cur.h;
+      const bool from = head && j >= up;
+      const int src = (int)(head ? (from ? l - up : l) : l);
+      const uint32_t moved = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * src, (int)s);
+      s = head ? (from ? moved : 0u) : s;
+      if (head && j == up) {
+        uint32_t x = UPD ? cur.state : kInit;
+        x = w8_unshift(x, cur.lead, lds);                                            // shift_{-lead}
+        x = byte_map64(byte_map64(x, lds, kLdsW8HalfOff), lds, kLdsW8HalfOff);       // shift_128
+        s ^= x;
+      }
+    }
+    if (__builtin_amdgcn_ballot_w64(last) != 0) {
+      const uint32_t t = group_xor_reduce<G>(w8_join(s, lds, j));
+      if (last && j == G - 1) {
+        const uint32_t over = 128 - cur.te;  // the last line's bytes past the payload end (zeroed above)
+        const uint32_t u = over ? w8_unshift(t, over, lds) : t;
+        out[cur.p] = UPD ? u : ~u;
+      }
+      s = last ? 0u : s;
+    }
+  };
+
+  auto step = [&](uint4 (&cur_buf)[8], uint4 (&nxt_buf)[8]) __attribute__((always_inline)) {
+    if (__builtin_amdgcn_ballot_w64(rL >= dL.R) != 0) {  // some group starts its next task
+      if (rL >= dL.R) {
+        tL += ngroups;
+        dL = decode_w8(rn, tL < t_end);
+        if constexpr (UPD) dL.state = dL.valid ? out[dL.p] : 0u;
+        rL = 0;
+      }
+    }
+    rn = raw(tL + ngroups);  // unconditional: the same address until dL ends
+    ANNETY_PRIO_HI();
+    load(dL, dL.valid ? rL : 0u, nxt_buf);
+    __builtin_amdgcn_sched_barrier(0);
+    ANNETY_PRIO_LO();
+    compute(cur_buf, dC, rC);
+    dC = dL;
+    rC = rL;
+    rL++;
+  };
+  // wave-uniform loop: the loads and the cross-lane steps need every group (a finished group reads a round of
+  // the class's last payload and stores nothing)
+  while (__builtin_amdgcn_ballot_w64(dC.valid) != 0) {
+    step(A, B);
+    step(B, A);
+  }
+}
+
+// The length-sorted path's class of payloads of <= 8 lines (round 5): one task = one payload = one round of a
+// lane group of 8 lanes. Lane j folds line j - (8 - nl) of the payload (end-aligned: the lanes before line 0
+// re-read line 0 and zero it) from register 0 with per-line loads; bytes before the payload start and past its
+// end are masked, the init (or the caller's register) enters as the register shift_{128-lead}(init) of line 0
+// (so 1-3 byte payloads and an init that spills into the second line need no case of their own), and the
+// group's join leaves the register at the last line's end, from which the inverse shift of the overhang gives
+// the payload's. Latency-bound (a descriptor, then at most 1 KiB of lines, per task): descriptors are fetched
+// two tasks ahead of their lines and the lines one task ahead of their fold, every load unconditional (a
+// finished group re-reads the class's last payload and stores nothing).
+//   STAGE as var_class: 1 = the whole var image with the G = 8 group part, 3 = the group part and the inverse
+//   shifts only (the common part is in place).
+struct S8Task {
+  uint64_t L0;  // the payload's first line (absolute 128-byte line index)
+  uint32_t nl, lead, te, p;
+  bool valid;
+};
+__device__ __forceinline__ S8Task decode_s8(uint4 d, bool valid) {
+  S8Task k;
+  const uint64_t a = ((uint64_t)d.y << 32) | d.x;
+  const uint64_t e = a + d.z;  // d.z > 0
+  k.L0 = a >> 7;
+  k.nl = (uint32_t)(((e - 1) >> 7) - k.L0 + 1);
+  k.lead = (uint32_t)(a & 127);
+  k.te = (uint32_t)(((e - 1) & 127) + 1);
+  k.p = d.w;
+  k.valid = valid;
+  return k;
+}
+template <bool UPD, int STAGE>
+__device__ __forceinline__ void var_class_s8(uint4* lds4, const uint8_t* __restrict__ base,
+                                             const uint4* __restrict__ desc, const uint32_t* __restrict__ range,
+                                             const uint4* __restrict__ img_slice, const uint4* __restrict__ img_g8,
+                                             const uint4* __restrict__ img_unshift, uint32_t* __restrict__ out) {
+  constexpr int G = 8;
+  const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
+  const uint32_t j = threadIdx.x & 7;
+  const size_t gid = group_id<kBlock, G, kVwg>();
+  const size_t ngroups = ((size_t)gridDim.x * kBlock) / G;
+  const size_t t_begin = range[0], t_end = range[1];
+  LaneCtx k;
+  k.L0 = (threadIdx.x & 31) << 3;
+  k.L1 = k.L0 | (1u << 16);
+  k.slot4 = (threadIdx.x & 31) << 2;                      // join slot: shift_{(7-j)*128}
+  const uint32_t slot128 = ((threadIdx.x & 31) | 6) << 2;  // the same replica's slot j = 6: shift_128
+  auto raw = [&](size_t t) { return raw_task<true>(t, t_end, base, desc, 0, 0); };
+  auto load = [&](const S8Task& tk, uint4 (&v)[8], uint32_t& st) __attribute__((always_inline)) {
+    const int32_t li = (int32_t)j - (int32_t)(8 - tk.nl);
+    const uint64_t src = (tk.L0 + (uint64_t)(li > 0 ? li : 0)) << 7;
+#pragma unroll
+    for (int i = 0; i < 8; i++) v[i] = gload16(src + 16 * i);
+    if constexpr (UPD) st = out[tk.p];
+  };
+
+  size_t t = t_begin + gid;  // the task computed this step
+  if (!__syncthreads_or(t < t_end)) {
+    if constexpr (STAGE == 1) {
+      load_image<kLdsVarImageBytes>(lds4, img_slice, img_g8, img_unshift);
+      __syncthreads();
+    }
+    return;
+  }
+  S8Task cur = decode_s8(raw(t), t < t_end);
+  uint4 A[8], B[8];
+  uint32_t stA = 0, stB = 0;
+  load(cur, A, stA);
+  uint4 d1 = raw(t + ngroups), d2 = raw(t + 2 * ngroups);  // the next two tasks' descriptors
+  if constexpr (STAGE == 3)
+    load_image<kLdsVarImageBytes, kBlock, kLdsImageBytes, kLdsCommonBytes>(lds4, img_slice, img_g8, img_unshift);
+  else
+    load_image<kLdsVarImageBytes>(lds4, img_slice, img_g8, img_unshift);
+  __syncthreads();
+
+  auto compute = [&](uint4 (&v)[8], const S8Task& tk, uint32_t st) __attribute__((always_inline)) {
+    const int32_t li = (int32_t)j - (int32_t)(8 - tk.nl);
+    const int32_t lo = li == 0 ? (int32_t)tk.lead : 0;
+    const int32_t hi = li < 0 ? 0 : (li == (int32_t)tk.nl - 1 ? (int32_t)tk.te : 128);
+    mask_line<8>(v, lo * 8, hi * 8);
+    uint32_t s = absorb_line(0u, v, k, lds);
+    if (li == 0) {  // the init as the register at the payload start: shift_{128-lead}(init) at line 0's end
+      uint32_t x = UPD ? st : kInit;
+      x = nibble_map_uniform(x, lds, kLdsUnshiftOff + (tk.lead & 15u) * 512);
+      x = nibble_map_uniform(x, lds, kLdsUnshiftOff + 8192 + (tk.lead >> 4) * 512);
+      s ^= nibble_map_lane(x, lds, slot128);
+    }
+    uint32_t r = group_xor_reduce<G>(nibble_map_lane(s, lds, k.slot4));
+    if (tk.valid && j == G - 1) {
+      const uint32_t over = 128 - tk.te;  // the last line's bytes past the payload end (zeroed above)
+      if (over) {
+        r = nibble_map_uniform(r, lds, kLdsUnshiftOff + (over & 15u) * 512);
+        r = nibble_map_uniform(r, lds, kLdsUnshiftOff + 8192 + (over >> 4) * 512);
+      }
+      out[tk.p] = UPD ? r : ~r;
+    }
+  };
+  auto step = [&](uint4 (&cur_buf)[8], uint32_t cur_st, uint4 (&nxt_buf)[8], uint32_t& nxt_st)
+      __attribute__((always_inline)) {
+    const uint4 d3 = raw(t + 3 * ngroups);  // unconditional (clamped past the end)
+    const S8Task nxt = decode_s8(d1, t + ngroups < t_end);
+    load(nxt, nxt_buf, nxt_st);
+    __builtin_amdgcn_sched_barrier(0);
+    compute(cur_buf, cur, cur_st);
+    cur = nxt;
+    t += ngroups;
+    d1 = d2;
+    d2 = d3;
+  };
+  while (__builtin_amdgcn_ballot_w64(cur.valid) != 0) {
+    step(A, stA, B, stB);
+    step(B, stB, A, stA);  // harmless when the group ran out of work on the first half: nothing is stored
+  }
+}
+
+// The sorted path in one launch (ranges[0..5] = the classes' [begin, end) in desc, longest first; crc32_bucket_place):
+// payloads of >= 9 lines (ranges[0..1]) run in var_class_w8, payloads of <= 8 lines (ranges[4..5]) in var_class_s8
+// (per-line loads, one round of 8 lanes each: latency-bound); ranges[2..3] is empty. Odd blocks run the
+// small class first, so that its dependent descriptor -> line -> fold steps overlap other blocks' streaming
+// instead of every block's tail (round 4, profiles/r04/sorted_nt/ab_class_order.log). The classes restage only
+// the part of the LDS image they do not share with the other.
+//   PROBE, classes: A/B builds only (microbench/sorted_probe.py); the product runs PROBE 0 and both classes.
+template <bool UPD, int PROBE = 0>
 __global__ __launch_bounds__(kBlock) void crc32_var_sorted_kernel(const uint8_t* __restrict__ base, size_t n,
                                                                   const uint4* __restrict__ desc,
                                                                   const uint32_t* __restrict__ ranges,
                                                                   const uint4* __restrict__ img_slice,
-                                                                  const uint4* __restrict__ img_g32,
-                                                                  const uint4* __restrict__ img_g16,
-                                                                  const uint4* __restrict__ img_g4,
+                                                                  const uint4* __restrict__ img_w8,
                                                                   const uint4* __restrict__ img_g8,
                                                                   const uint4* __restrict__ img_unshift,
                                                                   uint32_t* __restrict__ out, uint32_t classes) {
   __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsVarImageBytes / 16];
-  // classes: bit c runs class c (the product runs all three; the microbench timing of one class alone leaves
-  // digests of the others unwritten, ANNETY_CRC_SORTED_CLASSES); bit 3: the small class per line at G = 8, not 4;
-  // bit 4: odd blocks run the classes in reverse order (small, G = 16, G = 32), so that the small class's
-  // latency-bound steps overlap other blocks' streaming instead of all blocks' tails
-  if ((classes & 16) && (blockIdx.x & 1)) {
-    if (classes & 4)
-      var_class<4, true, UPD, kVwg, 0, 1>(lds4, base, n, 0, 0, desc, ranges + 4, img_slice, img_g4, img_unshift, out);
-    else
-      load_image<kLdsVarImageBytes>(lds4, img_slice, img_g4, img_unshift);
+  static_assert(kLdsW8ImageBytes <= kLdsVarImageBytes, "one LDS array serves both classes");
+  const uint32_t* none = ranges + 2;  // the empty middle range: a class switched off (A/B)
+  if (blockIdx.x & 1) {
+    var_class_s8<UPD, 1>(lds4, base, desc, classes & 2 ? ranges + 4 : none, img_slice, img_g8, img_unshift, out);
     __syncthreads();
-    if (classes & 2) {
-      if constexpr (NT & 2)
-        var_class_nt<16, UPD, 0>(lds4, base, desc, ranges + 2, img_slice, img_g16, img_unshift, out);
-      else
-        var_class<16, true, UPD, kVwg, 0, 0>(lds4, base, n, 0, 0, desc, ranges + 2, img_slice, img_g16, img_unshift, out);
-    }
-    __syncthreads();
-    if (classes & 1) {
-      if constexpr (NT & 1)
-        var_class_nt<32, UPD, 0>(lds4, base, desc, ranges, img_slice, img_g32, img_unshift, out);
-      else
-        var_class<32, true, UPD, kVwg, 0, 0>(lds4, base, n, 0, 0, desc, ranges, img_slice, img_g32, img_unshift, out);
-    }
-    return;
-  }
-  if (classes & 1) {
-    if constexpr (NT & 1)
-      var_class_nt<32, UPD, 1>(lds4, base, desc, ranges, img_slice, img_g32, img_unshift, out);
-    else
-      var_class<32, true, UPD, kVwg, 0, 1>(lds4, base, n, 0, 0, desc, ranges, img_slice, img_g32, img_unshift, out);
+    var_class_w8<UPD, 0, PROBE>(lds4, base, desc, classes & 1 ? ranges : none, img_slice, img_w8, out);
   } else {
-    load_image<kLdsVarImageBytes>(lds4, img_slice, img_g32, img_unshift);
+    var_class_w8<UPD, 1, PROBE>(lds4, base, desc, classes & 1 ? ranges : none, img_slice, img_w8, out);
+    __syncthreads();
+    var_class_s8<UPD, 3>(lds4, base, desc, classes & 2 ? ranges + 4 : none, img_slice, img_g8, img_unshift, out);
   }
-  __syncthreads();  // every wave is done with the G = 32 group tables
-  if (classes & 2) {
-    if constexpr (NT & 2)
-      var_class_nt<16, UPD, 0>(lds4, base, desc, ranges + 2, img_slice, img_g16, img_unshift, out);
-    else
-      var_class<16, true, UPD, kVwg, 0, 0>(lds4, base, n, 0, 0, desc, ranges + 2, img_slice, img_g16, img_unshift, out);
-  }
-  __syncthreads();
-  if (!(classes & 4)) return;
-  if constexpr (NT & 4)
-    var_class_nt8<UPD>(lds4, base, desc, ranges + 4, img_slice, img_g8, out);
-  else if (classes & 8)  // (A/B: the small class per line at G = 8)
-    var_class<8, true, UPD, kVwg, 0, 0>(lds4, base, n, 0, 0, desc, ranges + 4, img_slice, img_g8, img_unshift, out);
-  else
-    var_class<4, true, UPD, kVwg, 0, 0>(lds4, base, n, 0, 0, desc, ranges + 4, img_slice, img_g4, img_unshift, out);
 }
 
 // ---- long payloads: segments + CRC combine ----
@@ -1241,24 +1173,26 @@ hipError_t launch_fixed(const FixedLaunch& a, hipStream_t stream) {
   return a.full ? launch_full<true, false>(a, stream) : launch_full<false, false>(a, stream);
 }
 
-// the three classes, odd blocks in reverse order (A/B against 7: profiles/r04/sorted_nt/ab_class_order.log)
-constexpr uint32_t kSortedClassesDefault = 23;
-constexpr int kSortedNtDefault = 3;  // crc32_var_sorted_kernel NT: G = 32 and G = 16 coalesced (A/B against 1: profiles/r04/sorted_nt/ab_nt1_nt3.log)
-
-hipError_t launch_var_sorted(const VarLaunch& a, const void* img_g32, const void* img_g16, const void* img_g4,
-                             const void* img_g8, hipStream_t stream) {
+hipError_t launch_var_sorted(const VarLaunch& a, const void* img_w8, const void* img_g8, hipStream_t stream) {
   const unsigned blocks = (unsigned)std::max<size_t>(1, a.max_blocks);
   note_kernel("crc32_var_sorted_kernel");
-#define ANNETY_SORTED_LAUNCH(UPD, NT)                                                                         \
-  hipLaunchKernelGGL((crc32_var_sorted_kernel<UPD, NT>), dim3(blocks), dim3(kBlock), 0, stream,              \
+#define ANNETY_SORTED_LAUNCH(UPD, PROBE)                                                                      \
+  hipLaunchKernelGGL((crc32_var_sorted_kernel<UPD, PROBE>), dim3(blocks), dim3(kBlock), 0, stream,            \
                      static_cast<const uint8_t*>(a.base), a.n, static_cast<const uint4*>(a.desc), a.range,      \
-                     static_cast<const uint4*>(a.img_slice), static_cast<const uint4*>(img_g32),               \
-                     static_cast<const uint4*>(img_g16), static_cast<const uint4*>(img_g4),                    \
-                     static_cast<const uint4*>(img_g8),                                                         \
-                     static_cast<const uint4*>(a.img_unshift), a.out, classes)
-  constexpr uint32_t classes = kSortedClassesDefault;
-  if (a.update) ANNETY_SORTED_LAUNCH(true, kSortedNtDefault);
-  else ANNETY_SORTED_LAUNCH(false, kSortedNtDefault);
+                     static_cast<const uint4*>(a.img_slice), static_cast<const uint4*>(img_w8),                \
+                     static_cast<const uint4*>(img_g8), static_cast<const uint4*>(a.img_unshift), a.out, classes)
+#ifdef ANNETY_CRC_AB
+  static const uint32_t classes = (uint32_t)ANNETY_AB_KNOB("ANNETY_CRC_SORTED_CLASSES", 3);
+  static const int probe = ANNETY_AB_KNOB("ANNETY_CRC_W8_PROBE", 0);
+  if (!a.update && probe == 1) ANNETY_SORTED_LAUNCH(false, 1);
+  else if (!a.update && probe == 2) ANNETY_SORTED_LAUNCH(false, 2);
+  else if (a.update) ANNETY_SORTED_LAUNCH(true, 0);
+  else ANNETY_SORTED_LAUNCH(false, 0);
+#else
+  constexpr uint32_t classes = 3;
+  if (a.update) ANNETY_SORTED_LAUNCH(true, 0);
+  else ANNETY_SORTED_LAUNCH(false, 0);
+#endif
 #undef ANNETY_SORTED_LAUNCH
   return hipGetLastError();
 }

@@ -141,5 +141,18 @@ constexpr uint32_t kLdsQuarterOff = kLdsStitchUnshiftOff + kLdsUnshiftBytes;
 constexpr uint32_t kLdsMidOff = kLdsQuarterOff + 512;
 constexpr uint32_t kMidMaps = 6;  // P(2..7); P(1) = G(8) of the segment set, P(0) = identity
 constexpr uint32_t kLdsStitchImageBytes = kLdsMidOff + kMidMaps * 512;  // 163840: all of the CU's LDS
+// Length-sorted path, class of payloads of >= 9 lines (crc32_kernels.hip var_class_w8): common part, then the
+// device image "w8" (kW8ImgBytes):
+//   [kLdsW8JoinOff, +4 KiB)     lane-position join, unreplicated: (k, v, j) at (k*16 + v)*32 + j*4 =
+//                               shift_{(7-j)*128}(v << 4k) (used once per payload: bank conflicts are harmless)
+//   [kLdsW8HalfOff, +4 KiB)     byte tables of the half-line join shift_64 (crc32_device.h byte_map64)
+//   [kLdsW8RoundOff, +4 KiB)    byte tables of the round advance shift_{7*128}
+//   [kLdsW8UnshiftOff, +12 KiB) U_lo[m] = shift_{-m} (m = 0..15), U_hi[h] = shift_{-16h} (h = 0..7), 512 B each
+constexpr uint32_t kLdsW8JoinOff = kLdsCommonBytes;
+constexpr uint32_t kLdsW8HalfOff = kLdsW8JoinOff + 4096;
+constexpr uint32_t kLdsW8RoundOff = kLdsW8HalfOff + 4096;
+constexpr uint32_t kLdsW8UnshiftOff = kLdsW8RoundOff + 4096;
+constexpr uint32_t kLdsW8ImageBytes = kLdsW8UnshiftOff + kLdsUnshiftBytes;  // 156160
+constexpr uint32_t kW8ImgBytes = kLdsW8ImageBytes - kLdsCommonBytes;        // 24576
 
 }  // namespace annety_crc

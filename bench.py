@@ -44,6 +44,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.
 # gfx950 correction + WRITE_SIZE), committed per config; reported as `traffic` with the file as its source
 # (a PMC pass cannot run inside the timed process).
 PMC_FILES_VAR = {"sorted": "profiles/r04/config3_sorted_pmc.json"}  # config 3 on another variable path
+PMC_FILES_FRAMES = {}  # --config frames: (variant, op) -> committed PMC summary
 PMC_FILES = {1: "profiles/r04/config1_pmc.json", 3: "profiles/r04/config3_pmc.json",
              2: "profiles/r04/config2_pmc.json", 4: "profiles/r04/config1_pmc.json"}
 CPU_SAMPLE_BYTES = 1 << 30  # cpu_baseline sample: up to 1 GiB of the workload, far above the host's caches
@@ -53,14 +54,26 @@ REF_FLAGS = "g++ -std=c++11 -O2 -DNDEBUG (CMakeLists.txt:24,48 Release flags; -m
 
 def parse():
     p = argparse.ArgumentParser()
+    # (--config is parsed as text for "frames"; numeric configs become ints below)
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--prewarm-s", type=float, default=1.0,
                    help="untimed seconds of launches before warmup (the GPU ramps its clocks on sustained load)")
-    p.add_argument("--config", type=int, default=1, choices=[1, 2, 3, 4],
+    p.add_argument("--config", default="1", choices=["1", "2", "3", "4", "frames"],
                    help="BASELINE config: 1 = 1M x 1 KiB per GPU (default at every N), 2 = 4K x 4 MiB, "
-                        "3 = Zipf 64 B-64 KiB (~1 GiB), 4 = 8M x 1 KiB per GPU (config 4's shard) in chunks")
+                        "3 = Zipf 64 B-64 KiB (~1 GiB), 4 = 8M x 1 KiB per GPU (config 4's shard) in chunks; "
+                        "frames = annety's own frame regime (secondary line): a device-resident LengthHeaderCodec "
+                        "stream (4-byte lengths, checksum on), verified or encoded per step (--frames, --op)")
+    p.add_argument("--frames", choices=["mixed", "chat"], default="mixed",
+                   help="--config frames: mixed = payloads of 16 B-1 KiB (uniform); chat = 408 B payloads, the "
+                        "chat server's frames (examples/asio/chat/server/server.cc:25-27: LengthHeaderCodec(kLengthType32, "
+                        "checksum, max 408))")
+    p.add_argument("--op", choices=["verify", "encode"], default="verify",
+                   help="--config frames: verify = annety_lhc_verify_stream (LengthHeaderCodec::decode's checksum "
+                        "check over the received stream, include/codec/LengthHeaderCodec.h:100-136); encode = "
+                        "annety_lhc_encode_batch (LengthHeaderCodec::encode, :146-201)")
+    p.add_argument("--frames-n", type=int, default=2 << 20, help="--config frames: frames per step (default 2M)")
     p.add_argument("--strong", action="store_true",
                    help="fixed configs: --payloads (default 1M) is the TOTAL over all ranks, split into contiguous "
                         "shards (strong scaling); default is per GPU (weak scaling)")
@@ -104,7 +117,9 @@ def parse():
                    help="check only a 4 MiB prefix of the batch against the oracle before timing (default: every "
                         "digest, 1 GiB at a time)")
     p.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample duration")
-    return p.parse_args()
+    a = p.parse_args()
+    a.config = int(a.config) if a.config.isdigit() else a.config
+    return a
 
 
 def _free_port() -> int:
@@ -176,7 +191,7 @@ class Workload:
         self.torch = torch
         self.dev = dev
         gen = torch.Generator(device=dev)
-        gen.manual_seed(0xC0FFEE + 7919 * rank + args.config)
+        gen.manual_seed(0xC0FFEE + 7919 * rank + (args.config if isinstance(args.config, int) else 5))
         self.config = args.config
         self.arena = False
         if args.config in (1, 2, 4):
@@ -207,6 +222,8 @@ class Workload:
             else:
                 self.desc = (f"BASELINE config {args.config}: {n} x {L} B payloads contiguous in HBM per GPU, "
                              "one batch launch per step")
+        elif args.config == "frames":
+            self._init_frames(args, dev, rank, gen)
         else:
             lens, offs = zipf_batch(0x5EED + rank)
             total = int(lens.sum())
@@ -232,10 +249,107 @@ class Workload:
         self._fixed = _lib.get().annety_crc32_batch_fixed
         self._data_ptr = self.data.data_ptr()
 
+    def _init_frames(self, args, dev, rank, gen):
+        """--config frames: n payloads (16 B-1 KiB uniform, or all 408 B) packed in a source buffer, and the
+        LengthHeaderCodec stream of them (4-byte big-endian length = payload + 4, payload, big-endian CRC),
+        built on the device by the library's encoder and checked against the oracle before timing."""
+        import torch
+
+        import annety_amd
+
+        torch = self.torch
+        rng = np.random.default_rng(0xF4A3E5 + rank)
+        n = args.frames_n
+        lens = (np.full(n, 408, dtype=np.int64) if args.frames == "chat" else rng.integers(16, 1025, n))
+        src_off = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+        total = int(lens.sum())
+        self.src = torch.randint(0, 256, (total,), dtype=torch.uint8, device=dev, generator=gen)
+        self.codec = annety_amd.LengthHeaderCodec(4, True, 1 << 20)
+        enc = self.codec.encode_batch(self.src, src_off.astype(np.uint64), lens.astype(np.uint32))
+        torch.cuda.synchronize()
+        self.frame_off = enc.frame_off
+        self.stream = enc.frames  # the received stream of the verify step; the encode step rewrites a copy
+        self.n, self.L = n, None
+        self.n_total = n
+        self.lens_host, self.src_off_host = lens, src_off
+        self.payload_bytes = total
+        self.op = args.op
+        self.frames_variant = args.frames
+        self.d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
+        if args.op == "verify":
+            self.offsets = torch.from_numpy(enc.frame_off.astype(np.int64) + 4).to(dev)  # payloads in the stream
+            self.ok = torch.zeros(n, dtype=torch.uint8, device=dev)
+            # payload reads + trailer reads + offset/length reads + verdict and digest writes, per frame
+            self.algo_bytes = total + n * (4 + 12 + 1 + 4)
+        else:
+            self.offsets = torch.from_numpy(src_off).to(dev)  # payloads in the source buffer
+            self.d_foff = torch.from_numpy(enc.frame_off.astype(np.int64)).to(dev)
+            self.frames_out = torch.empty_like(self.stream)
+            # payload reads + frame writes (header + payload + trailer) + src/frame offset and length reads
+            self.algo_bytes = 2 * total + n * (8 + 20)
+        self.lengths = self.d_len
+        kind = "16 B-1 KiB uniform" if args.frames == "mixed" else "408 B (the chat server's MSS)"
+        self.desc = (f"annety frames ({args.frames}): {n} LengthHeaderCodec frames (4-byte lengths, checksum), payloads "
+                     f"{kind}, {total / 2**30:.3f} GiB of payload, device-resident; one "
+                     + ("annety_lhc_verify_stream (CRC of every payload against its trailer)" if args.op == "verify"
+                        else "annety_lhc_encode_batch (header, payload copy, CRC trailer)") + " per step")
+
+    def frames_check(self) -> dict:
+        """Every frame of the step's output against the oracle: verify - every verdict 1 and every digest the
+        oracle's; encode - the whole output stream byte for byte against the stream the reference's framing
+        gives (header, payload, big-endian oracle CRC)."""
+        import oracle
+
+        torch = self.torch
+        t0 = time.perf_counter()
+        host = self.src.cpu().numpy()
+        want = oracle.batch_var_mt(host, self.src_off_host.astype(np.uint64), self.lens_host.astype(np.uint32),
+                                   threads=min(16, os.cpu_count() or 1))
+        if self.op == "verify":
+            if not bool((self.ok == 1).all()):
+                raise SystemExit("frames: a verdict is not 1")
+            if not np.array_equal(self.out.cpu().numpy().view(np.uint32), want):
+                raise SystemExit("frames: digests differ from the oracle")
+        else:
+            got = self.frames_out.cpu().numpy()
+            exp = np.empty_like(got)
+            fo = self.frame_off.astype(np.int64)
+            L = self.lens_host
+            hdr = (L + 4).astype(np.uint32)
+            for k in range(4):
+                exp[fo + k] = (hdr >> (8 * (3 - k))) & 0xFF
+                exp[fo + 4 + L + k] = (want >> (8 * (3 - k))) & 0xFF
+            # payload bytes: one vectorised gather per frame position
+            idx = np.repeat(fo + 4 - self.src_off_host, L) + np.arange(int(L.sum()))
+            exp[idx] = host
+            if not np.array_equal(got, exp):
+                raise SystemExit(f"frames: encoded stream differs at byte {int(np.flatnonzero(got != exp)[0])}")
+        torch.cuda.synchronize()
+        return {"frames": self.n, "against": "oracle (C restatement pinned by tests/golden)",
+                "seconds": round(time.perf_counter() - t0, 2)}
+
     def launch(self, stream_handle, lo: int = 0, hi: int | None = None):
         """Digests of payloads [lo, hi) into self.out[lo:hi] (fixed configs); the whole batch otherwise."""
         import annety_amd
         from annety_amd import _lib
+
+        if self.config == "frames":
+            lib = _lib.get()
+            if self.op == "verify":
+                st = lib.annety_lhc_verify_stream(self.stream.data_ptr(), self.stream.numel(), self.offsets.data_ptr(),
+                                                  self.d_len.data_ptr(), self.n, self.ok.data_ptr(),
+                                                  self.out.data_ptr(), stream_handle)
+                name = "annety_lhc_verify_stream"
+            else:
+                st = lib.annety_lhc_encode_batch(self.src.data_ptr(), self.offsets.data_ptr(), self.d_len.data_ptr(),
+                                                 self.n, 4, 1 << 20, self.frames_out.data_ptr(), self.d_foff.data_ptr(),
+                                                 stream_handle)
+                name = "annety_lhc_encode_batch"
+            if st:
+                _lib.check(st, name)
+            if self.kernel is None:
+                self.kernel = annety_amd.last_kernels()
+            return self.out
 
         if self.config in (1, 2, 4):
             hi = self.n_pad if hi is None else hi
@@ -258,6 +372,11 @@ class Workload:
 
     def host_sample(self, max_bytes=4 << 20):
         """(host bytes, offsets, lengths) of a bounded prefix of the batch, for the oracle legs."""
+        if self.config == "frames":  # the payloads, as the CPU codec would checksum them
+            end = np.cumsum(self.lens_host)
+            ns = max(1, int(np.searchsorted(end, max_bytes)))
+            h = self.src[: int(end[ns - 1])].cpu().numpy()
+            return h, self.src_off_host[:ns].astype(np.uint64), self.lens_host[:ns].astype(np.uint32)
         if self.config in (1, 2, 4):
             ns = max(1, min(self.n, max_bytes // self.L))
             h = self.data[: ns * self.L].cpu().numpy()
@@ -377,6 +496,8 @@ def pmc_traffic(w: Workload, var_path: str):
     path = PMC_FILES.get(w.config)
     if w.config == 3 and var_path != "arena":
         path = PMC_FILES_VAR.get(var_path)
+    if w.config == "frames":
+        path = PMC_FILES_FRAMES.get((w.frames_variant, w.op))
     if not path or (w.config in (1, 4) and w.L != 1024):
         return None
     try:
@@ -384,7 +505,7 @@ def pmc_traffic(w: Workload, var_path: str):
             d = json.load(f)
     except (OSError, ValueError):
         return None
-    tot = sum(v.get("hbm_bytes_per_launch", 0) for k, v in d.items() if "crc32_" in k)
+    tot = sum(v.get("hbm_bytes_per_launch", 0) for k, v in d.items() if "crc32_" in k or "lhc_" in k)
     if not tot:
         return None
     if w.config == 4:  # the config-1 measurement is per 1M payloads; a config-4 step is n/1M of them
@@ -475,6 +596,8 @@ def main():
         args.chunks = 2 if args.config == 4 else 1
     if args.var_path in ("sorted", "auto"):
         os.environ["ANNETY_CRC_VAR_PATH"] = args.var_path  # read once by the library: before it loads
+    if args.config == "frames" and multi:
+        raise SystemExit("--config frames is a one-GPU secondary line")
     if multi and int(os.environ.get("GPU_MAX_HW_QUEUES", "4")) < args.hw_queues:
         # HIP maps streams onto GPU_MAX_HW_QUEUES hardware queues (4 by default); the compute stream, torch's
         # RCCL stream and RCCL's own streams then share queues, and a queue runs its packets in order. Set
@@ -544,13 +667,16 @@ def main():
     # every rank's digests delivered to rank 0 intact (checksum of checksums)
     sharded.PipelinedGather.wait(step())
     torch.cuda.synchronize()
-    hs, ho, hl = w.host_sample()
-    want = oracle.batch_var(hs, ho, hl)
     steady_kernels = w.kernel
-    got = w.out[: len(ho)].cpu().numpy().view(np.uint32)
-    if not np.array_equal(got, want):
-        raise SystemExit(f"rank {rank}: digests differ from the oracle on the sample")
-    checked = full_check(w, threads=min(16, os.cpu_count() or 1)) if not args.sample_check else None
+    if w.config == "frames":
+        checked = w.frames_check()
+    else:
+        hs, ho, hl = w.host_sample()
+        want = oracle.batch_var(hs, ho, hl)
+        got = w.out[: len(ho)].cpu().numpy().view(np.uint32)
+        if not np.array_equal(got, want):
+            raise SystemExit(f"rank {rank}: digests differ from the oracle on the sample")
+        checked = full_check(w, threads=min(16, os.cpu_count() or 1)) if not args.sample_check else None
     gather_ok = sharded.verify_gather(pipe.recv, w.out) if pipe is not None else None
     if gather_ok is False:
         raise SystemExit(f"rank {rank}: gathered digests differ from the ranks' own")
@@ -616,6 +742,8 @@ def main():
         elif args.config == 4:
             metric = METRIC.replace("(1M×1KiB)", "(8M×1KiB per GPU, config 4)" if not args.strong
                                     else "(8M×1KiB total, config 4, strong scaling)")
+        elif args.config == "frames":
+            metric = METRIC.replace("(1M×1KiB)", f"(annety frames, {args.frames}, {args.op})")
         else:
             metric = METRIC.replace("(1M×1KiB)", f"(config {args.config})")
         line = {
@@ -640,7 +768,7 @@ def main():
                 "workload": w.desc,
                 "payloads_per_gpu": w.n,
                 "payloads_total": w.n_total,
-                "payload_bytes": w.L if w.L else "zipf",
+                "payload_bytes": w.L if w.L else ("zipf" if w.config == 3 else args.frames),
                 "bytes_per_gpu": w.payload_bytes,
                 "parallelism": f"shard{world}" if multi else "single",
             },

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define ANNETY_CRC_ABI_VERSION 4
+#define ANNETY_CRC_ABI_VERSION 5
 
 enum {
   ANNETY_CRC_OK = 0,

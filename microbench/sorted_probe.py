@@ -1,0 +1,73 @@
+#!/usr/bin/env python3
+"""Stage costs of the length-sorted path on BASELINE config 3, with the A/B build of the library
+(python -m annety_amd.build --ab -> microbench/libannety_crc_ab.so, loaded through ANNETY_CRC_LIB). Each setting
+runs in a child process (the library reads its switches once):
+  ANNETY_CRC_SORTED_CLASSES: bit 0 = the >= 9-line class (var_class_w8), bit 1 = the <= 8-line class
+  ANNETY_CRC_W8_PROBE: 1 = every step unmasked, 2 = no fold (wrong digests)
+Per setting: microseconds per crc32_batch_var call (HIP events over 200 calls, median of 5 groups), alternating
+settings twice. Usage: python microbench/sorted_probe.py [settings...], a setting = "classes:probe" (default:
+3:0 1:0 2:0 3:1 3:2)."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def child():
+    import numpy as np
+    import torch
+
+    import annety_amd
+    import bench
+
+    dev = torch.device("cuda", 0)
+    lens, offs = bench.zipf_batch(0x5EED)
+    if os.environ.get("PROBE_BATCH") == "small":  # 2M frames of 16 B - 1 KiB, shuffled
+        rng = np.random.default_rng(7)
+        lens = rng.integers(16, 1025, 2 << 20)
+        offs = np.concatenate([[0], np.cumsum(lens)[:-1]])
+    g = torch.Generator(device=dev)
+    g.manual_seed(4242)
+    data = torch.randint(0, 256, (int(lens.sum()),), dtype=torch.uint8, device=dev, generator=g)
+    d_off = torch.from_numpy(offs.astype(np.int64)).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
+    annety_amd.set_var_path("sorted")
+    out = torch.empty(len(lens), dtype=torch.int32, device=dev)
+    for _ in range(20):
+        annety_amd.crc32_batch_var(data, d_off, d_len, out=out)
+    torch.cuda.synchronize()
+    per = []
+    for _ in range(5):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(200):
+            annety_amd.crc32_batch_var(data, d_off, d_len, out=out)
+        e1.record()
+        torch.cuda.synchronize()
+        per.append(e0.elapsed_time(e1) / 200 * 1e3)
+    print(json.dumps({"us": sorted(per)[2], "kernels": annety_amd.last_kernels()}))
+
+
+def main():
+    if os.environ.get("SORTED_PROBE_CHILD"):
+        return child()
+    settings = sys.argv[1:] or ["3:0", "1:0", "2:0", "3:1", "3:2"]
+    lib = os.path.join(ROOT, "microbench", "libannety_crc_ab.so")
+    for rep in range(2):
+        for st in settings:
+            cl, pr = st.split(":")
+            env = dict(os.environ, SORTED_PROBE_CHILD="1", ANNETY_CRC_LIB=lib, ANNETY_CRC_SORTED_CLASSES=cl,
+                       ANNETY_CRC_W8_PROBE=pr)
+            r = subprocess.run([sys.executable, os.path.abspath(__file__)], env=env, capture_output=True, text=True,
+                               timeout=300)
+            line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+            res = json.loads(line[-1]) if line else {"error": r.stderr[-500:]}
+            print(f"rep {rep} classes {cl} probe {pr}: {res}", flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

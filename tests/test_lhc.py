@@ -204,6 +204,32 @@ def test_gpu_encode_decode_round_trip_and_corruption(gpu):
         assert int((e.ok == 0).sum()) == 1
 
 
+@pytest.mark.gpu
+def test_gpu_encode_fused_every_alignment(gpu):
+    """The one-pass encoder (crc32_frames.hip lhc_encode_fused_kernel) at every edge its copy has: payload lengths
+    0..300 (empty frames write nothing; 1-3 byte payloads are all edge bytes), source starts at every offset of
+    a 128-byte line, destination alignments from the packed frames of every header width, payloads that end in
+    the first bytes of a line (the copy's dword straddling two lines), and lengths just around whole lines and
+    whole 8-line rounds; every frame against the oracle's encoder."""
+    import torch
+
+    rng = np.random.default_rng(20261018)
+    lens = np.concatenate([np.arange(0, 301), rng.integers(0, 3000, 400),
+                           np.array([128 * k + d for k in (1, 7, 8, 9, 15, 16, 17, 64) for d in (-5, -1, 0, 1, 3)])])
+    lens = rng.permutation(lens).astype(np.uint32)
+    starts = rng.integers(0, 128, lens.size)
+    offs = (np.arange(lens.size, dtype=np.uint64) * 4096 + starts.astype(np.uint64)).astype(np.uint64)
+    arena = oracle.lcg_bytes(int(offs[-1]) + 4096 + 8, 123)
+    d_src = torch.from_numpy(arena.copy()).to(gpu)
+    for T in (1, 2, 4, 8):
+        codec = LengthHeaderCodec(T, True, 4000 if T > 1 else 200)
+        r = codec.encode_batch(d_src, offs, lens)
+        frames = r.frames.cpu().numpy().tobytes()
+        want = b"".join(oracle.lhc_encode(arena[int(o): int(o) + int(L)], T, codec.max_payload)[1]
+                        for o, L in zip(offs, lens))
+        assert frames == want, T
+
+
 # ---------------- the reference codec itself, linked against the drop-in ----------------
 @pytest.mark.skipif(not os.path.isdir("/root/reference/src"), reason="reference tree not present")
 def test_reference_codec_runs_on_dropin(golden, tmp_path):
