@@ -615,7 +615,7 @@ __global__ __launch_bounds__(kBucketThreads) void crc32_bucket_place(const uint6
   if (blockIdx.x == 0) {
     bk.cursor_next[t] = 0u;
     // classes by line count (bucket = 1023 - lines): >= 9 lines (crc32_kernels.hip var_class_w8), an empty
-    // middle range, <= 8 lines (var_class<4>)
+    // middle range, <= 8 lines (var_class_s8)
     constexpr uint32_t b16 = kBucketCount - 9, b4 = kBucketCount - 9;  // bucket 1015 = 8 lines
     if (t == 0) bk.ranges[0] = 0u;
     if (t == b16) bk.ranges[1] = bk.ranges[2] = start;

@@ -537,7 +537,7 @@ int scratch_done(DeviceCtx& c, ScratchSlot* slot) {
 // after it.
 size_t sorted_scratch_bytes(size_t n) {
   const size_t rows_words = (size_t)bucket_grid(n) * kBucketCount;
-  return (rows_words + 8) * sizeof(uint32_t) + 16 * n;  // rows + ranges (16-byte multiple) + descriptors
+  return (rows_words + kRangeWords) * sizeof(uint32_t) + 16 * n;  // rows + ranges and counters + descriptors
 }
 
 // The length classes in one launch (the product) or one launch each (A/B builds: ANNETY_CRC_SORTED_FUSED=0).
@@ -563,7 +563,7 @@ int run_var_sorted_in(DeviceCtx& c, ScratchSlot* slot, const void* d_base, size_
   bk.base = d_base;
   bk.rows = reinterpret_cast<uint32_t*>(scratch);
   bk.ranges = bk.rows + rows_words;
-  bk.desc = scratch + (rows_words + 8) * sizeof(uint32_t);
+  bk.desc = scratch + (rows_words + kRangeWords) * sizeof(uint32_t);
   const uint32_t set = (uint32_t)(slot->data.sorts & 1);
   bk.cursor = cursors + set * kBucketCount;
   bk.cursor_next = cursors + (set ^ 1) * kBucketCount;

@@ -89,7 +89,7 @@ __global__ __launch_bounds__(kBlock) void lhc_encode_fused_kernel(const uint8_t*
   k.L0 = (threadIdx.x & 31) << 3;
   k.L1 = k.L0 | (1u << 16);
   k.slot4 = (threadIdx.x & 31) << 2;
-  const uint32_t slot128 = ((threadIdx.x & 31) | 6) << 2;  // shift_128 (join slot j = 6)
+  const uint32_t slot128 = ((threadIdx.x & 24) | 6) << 2;  // shift_128 (join slot j = 6 of this replica row)
   auto fetch = [&](size_t t, uint64_t& so, uint32_t& ln, uint64_t& fo) __attribute__((always_inline)) {
     const size_t tc = t < n ? t : n - 1;  // unconditional: past the end re-read the last frame's fields
     so = src_off[tc];

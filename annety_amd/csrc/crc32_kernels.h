@@ -139,12 +139,14 @@ constexpr uint32_t kBucketThreads = 1024;  // both launches; one payload per thr
 constexpr size_t kCursorOff = 8192;        // the two cursor sets, in the extent scratch (2 x 4 KiB)
 static_assert((8 + 4 * kExtentMaxParts) * 8 <= kCursorOff && kCursorOff + 2 * 4 * kBucketCount <= kExtentScratchBytes,
               "extent scratch layout");
+// The ranges area (BucketArgs::ranges): the classes' bounds and two spare words
+constexpr uint32_t kRangeWords = 8;
 struct BucketArgs {
   const void* base;       // payload offsets are relative to this pointer
   uint32_t* rows;         // bucket_grid(n) * kBucketCount words
   uint32_t* cursor;       // this call's set (zero on entry)
   uint32_t* cursor_next;  // the other set: zeroed by launch_bucket_place
-  uint32_t* ranges;       // 6 words: {begin, end} of the G = 32 / 16 / 4 classes in desc
+  uint32_t* ranges;       // kRangeWords: {begin, end} of the classes (>= 9 lines, empty, <= 8 lines) in desc
   void* desc;             // uint4 {addr lo, addr hi, len, index} per non-empty payload
   uint32_t* out;          // zero-length digests; null in update mode
 };

@@ -640,8 +640,14 @@ __global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __rest
 // The wave's 8 groups take 8 consecutive tasks of the length-sorted list (equal line counts in the same
 // bucket), so they start and finish together: every step in which no group is in its head or last round (or
 // idle) takes the unmasked branch, wave-uniformly; the rest (about 2 per 8 payloads, 15 % of config 3's steps)
-// take the masked one. Groups still step through their own task sequences (t += number of groups), so unequal
-// lengths never idle a group.
+// take the masked one.
+// Scheduling: a wave takes SETS of 8 consecutive tasks, one per group, and moves to its next set when all 8 are
+// done (equal lengths inside a bucket: the lockstep idles 0.02 % of config 3's group rounds). Blocks own the sets in
+// snake order over the sorted list, and a block's waves take its sets longest first, each to the wave that frees up
+// first (an LDS counter, claimed 3 steps before the switch): the busiest wave of config 3 holds 67 rounds against a
+// mean of 65.3. Static round-robin over the sorted list gave every long set of each row to the same few waves (103
+// rounds: 0.63 of the ideal; snake order over waves 74), and a chip-wide counter in HBM cost more than it saved
+// (its atomics serialise: DESIGN.md §2.5).
 struct W8Task {
   uint64_t a0;  // address of the payload's first line (128-aligned)
   uint32_t lead, te, h, R, p, state;
@@ -680,8 +686,10 @@ __device__ __forceinline__ uint32_t w8_join(uint32_t s, const uint32_t* lds, uin
 //   STAGE: 1 = stage the whole image (also for a block without work of this class), 0 = only the w8 part (the
 //   common part is in place).
 //   PROBE (A/B builds only, microbench/sorted_probe.py; product = 0): bit 0 = every step takes the unmasked
-//   branch, bit 1 = no fold (the data are xored into the register) - wrong digests, used to measure what the
-//   masked rounds and the fold cost.
+//   branch, bit 1 = no fold (the data are xored into the register), bit 2 = loads from config 1's window (wave w,
+//   step s: 8 KiB at (s W + w) 8 KiB) instead of the tasks' rounds, bit 3 = the same window loaded with config 1's
+//   scalar base and immediate offsets - wrong digests, used to measure what the masked rounds, the fold, the
+//   access pattern and the per-group addressing cost.
 template <bool UPD, int STAGE, int PROBE = 0>
 __device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restrict__ base,
                                              const uint4* __restrict__ desc, const uint32_t* __restrict__ range,
@@ -704,8 +712,22 @@ __device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restr
   // transpose_blocks lane l holds half l3 of line j of the even group of its pair (l >> 3 & ~1) in v[0..3] and of
   // the odd one in v[4..7] (crc32_onekib_nt_kernel's layout). Invalid groups decode the last task of the class
   // (raw_task clamps), so every address is inside a payload of >= 9 lines.
+  uint32_t wstep = 0;  // steps so far (PROBE bits 2, 3)
   auto load = [&](const W8Task& tk, uint32_t r, uint4 (&v)[8]) __attribute__((always_inline)) {
-    const uint64_t ad = tk.a0 + (r == 0 ? 0ull : (uint64_t)tk.h * 128u + (uint64_t)(r - 1) * 1024u);
+    uint64_t ad = tk.a0 + (r == 0 ? 0ull : (uint64_t)tk.h * 128u + (uint64_t)(r - 1) * 1024u);
+    if constexpr ((PROBE & 4) != 0)  // config 1's window instead of the tasks' rounds (wrong digests)
+      ad = b0 + ((((uint64_t)wstep * (ngroups / 8) + (gid >> 3)) * 8192 + 1024 * (l >> 3)) & ((1ull << 29) - 1));
+    if constexpr ((PROBE & 8) != 0) {  // the same window with config 1's scalar base + immediate offsets
+      const uint64_t wb = ((((uint64_t)wstep * (ngroups / 8) + (uint32_t)__builtin_amdgcn_readfirstlane((int)(gid >> 3))) *
+                           8192) & ((1ull << 29) - 1));
+      const uint8_t* p = base + wb + voff;
+#pragma unroll
+      for (int i = 0; i < 8; i++) {
+        const v4u32 x = __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(p + 1024 * i));
+        v[i] = make_uint4(x.x, x.y, x.z, x.w);
+      }
+      return;
+    }
     const uint32_t lo = (uint32_t)ad, hi = (uint32_t)(ad >> 32);
 #pragma unroll
     for (int i = 0; i < 8; i++) {
@@ -718,32 +740,44 @@ __device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restr
     }
   };
 
-  size_t t0 = t_begin + gid;
-  if (!__syncthreads_or(t0 < t_end)) {  // the block has no task of this class
+  // Sets: block b owns the sets k NB + b (k even) and k NB + NB - 1 - b (k odd), NB = the grid's blocks (snake
+  // order over the sorted list, so every block gets an even share of long and short sets); its 8 waves take them
+  // in list order, wave w the w-th first, every later one from a counter in LDS when the wave's set is 3 steps from
+  // its end (the descriptors come from HBM in the meantime): longest first, each to the wave that frees up first.
+  __shared__ uint32_t sets_taken;
+  const uint32_t nb = gridDim.x, bb = blockIdx.x, m = l >> 3;
+  const uint32_t nsets = (uint32_t)((t_end - t_begin + 7) / 8);
+  auto set_of = [&](uint32_t kk) {
+    const uint64_t g = (uint64_t)kk * nb + ((kk & 1u) ? nb - 1 - bb : bb);
+    return g < nsets ? (uint32_t)g : nsets;  // nsets: no set (every task_of >= t_end)
+  };
+  auto task_of = [&](uint32_t set) { return t_begin + 8 * (size_t)set + m; };
+  uint32_t S0 = set_of(threadIdx.x >> 6);  // the set being loaded; S1, the next one (descriptors in rn), below
+  if (!__syncthreads_or(task_of(S0) < t_end)) {  // the block has no task of this class
     if constexpr (STAGE == 1) {
       load_image<kLdsW8ImageBytes, kBlock, kLdsCommonBytes>(lds4, img_slice, nullptr, img_w8);
       __syncthreads();
     }
     return;
   }
-  // Pipeline: the load side holds the task whose round rL it loads this step (dL, index tL) and the raw
-  // descriptor of the task after it (rn), fetched every step from the same address while dL runs: when dL
-  // ends, rn was first requested a whole task earlier and the decode never waits on HBM (fetching only the
-  // next step's descriptor, as var_class does, exposed a miss at every task switch: 205 us for the loads
-  // and the bookkeeping alone on config 3). The compute side (dC, rC) is the load side one step later.
-  W8Task dL = decode_w8(raw(t0), t0 < t_end);
+  // Pipeline: the load side holds the task whose round rL it loads this step (dL); rn is the raw descriptor of
+  // this group's task in the next set, fetched every other step from the same address (a claim comes at least
+  // two steps before its switch), so a switch never waits on HBM. The compute side (dC, rC) is the load side one
+  // step later.
+  W8Task dL = decode_w8(raw(task_of(S0)), task_of(S0) < t_end);
   if constexpr (UPD) dL.state = dL.valid ? out[dL.p] : 0u;
-  size_t tL = t0;
-  uint4 rn = raw(tL + ngroups);
-
   uint4 A[8], B[8];
   load(dL, 0, A);
+  uint32_t S1 = nsets;  // not claimed yet
+  bool claimed = false;
+  uint4 rn = raw(task_of(S1));
   W8Task dC = dL;
   uint32_t rC = 0, rL = 1;
   if constexpr (STAGE == 0)
     load_image<kLdsW8ImageBytes, kBlock, kLdsCommonBytes, kLdsCommonBytes>(lds4, img_slice, nullptr, img_w8);
   else
     load_image<kLdsW8ImageBytes, kBlock, kLdsCommonBytes>(lds4, img_slice, nullptr, img_w8);
+  if (threadIdx.x == 0) sets_taken = kBlock / 64;
   __syncthreads();
 
   uint32_t s = 0;
@@ -756,9 +790,11 @@ __device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restr
     v[4].x ^= l3 ? 0u : sp;
     s = fold_halves(v, k, lds, l3, kLdsW8HalfOff);
   };
-  auto compute = [&](uint4 (&v)[8], const W8Task& cur, uint32_t r_c) __attribute__((always_inline)) {
-    transpose_blocks(v);
+  auto compute = [&](uint4 (&v)[8], W8Task cur, uint32_t r_c) __attribute__((always_inline)) {
+    cur.valid = cur.valid && r_c < cur.R;
     const bool body = cur.valid && r_c > 0 && r_c + 1 < cur.R;
+    transpose_blocks(v);
+    // (a group that finished its task before the rest of its set idles: r_c >= R, treated as invalid)
     if constexpr ((PROBE & 2) != 0) {
       uint32_t x = s;
 #pragma unroll
@@ -824,30 +860,38 @@ __device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restr
     }
   };
 
-  auto step = [&](uint4 (&cur_buf)[8], uint4 (&nxt_buf)[8]) __attribute__((always_inline)) {
-    if (__builtin_amdgcn_ballot_w64(rL >= dL.R) != 0) {  // some group starts its next task
-      if (rL >= dL.R) {
-        tL += ngroups;
-        dL = decode_w8(rn, tL < t_end);
+  auto step = [&](uint4 (&cur_buf)[8], uint4 (&nxt_buf)[8], bool fetch) __attribute__((always_inline)) {
+    if (__builtin_amdgcn_ballot_w64(rL + 3 < dL.R) == 0) {  // every group of the wave is within 3 steps of its end
+      if (!claimed) {  // (wave-uniform) the next set from the block's counter
+        uint32_t kk = 0;
+        if (l == 0) kk = __hip_atomic_fetch_add(&sets_taken, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        S1 = set_of((uint32_t)__builtin_amdgcn_readfirstlane((int)kk));
+        claimed = fetch = true;
+      }
+      if (__builtin_amdgcn_ballot_w64(rL < dL.R) == 0) {  // every group is done with S0: switch
+        S0 = S1;
+        claimed = false;
+        dL = decode_w8(rn, task_of(S0) < t_end);
         if constexpr (UPD) dL.state = dL.valid ? out[dL.p] : 0u;
         rL = 0;
       }
     }
-    rn = raw(tL + ngroups);  // unconditional: the same address until dL ends
+    if (fetch) rn = raw(task_of(S1));
     ANNETY_PRIO_HI();
-    load(dL, dL.valid ? rL : 0u, nxt_buf);
+    load(dL, dL.valid && rL < dL.R ? rL : 0u, nxt_buf);
     __builtin_amdgcn_sched_barrier(0);
     ANNETY_PRIO_LO();
     compute(cur_buf, dC, rC);
     dC = dL;
     rC = rL;
     rL++;
+    wstep++;
   };
   // wave-uniform loop: the loads and the cross-lane steps need every group (a finished group reads a round of
   // the class's last payload and stores nothing)
   while (__builtin_amdgcn_ballot_w64(dC.valid) != 0) {
-    step(A, B);
-    step(B, A);
+    step(A, B, true);
+    step(B, A, false);
   }
 }
 
@@ -894,7 +938,7 @@ __device__ __forceinline__ void var_class_s8(uint4* lds4, const uint8_t* __restr
   k.L0 = (threadIdx.x & 31) << 3;
   k.L1 = k.L0 | (1u << 16);
   k.slot4 = (threadIdx.x & 31) << 2;                      // join slot: shift_{(7-j)*128}
-  const uint32_t slot128 = ((threadIdx.x & 31) | 6) << 2;  // the same replica's slot j = 6: shift_128
+  const uint32_t slot128 = ((threadIdx.x & 24) | 6) << 2;  // this replica row's slot j = 6: shift_128
   auto raw = [&](size_t t) { return raw_task<true>(t, t_end, base, desc, 0, 0); };
   auto load = [&](const S8Task& tk, uint4 (&v)[8], uint32_t& st) __attribute__((always_inline)) {
     const int32_t li = (int32_t)j - (int32_t)(8 - tk.nl);
@@ -1186,6 +1230,9 @@ hipError_t launch_var_sorted(const VarLaunch& a, const void* img_w8, const void*
   static const int probe = ANNETY_AB_KNOB("ANNETY_CRC_W8_PROBE", 0);
   if (!a.update && probe == 1) ANNETY_SORTED_LAUNCH(false, 1);
   else if (!a.update && probe == 2) ANNETY_SORTED_LAUNCH(false, 2);
+  else if (!a.update && probe == 6) ANNETY_SORTED_LAUNCH(false, 6);
+  else if (!a.update && probe == 10) ANNETY_SORTED_LAUNCH(false, 10);
+  else if (!a.update && probe == 8) ANNETY_SORTED_LAUNCH(false, 8);
   else if (a.update) ANNETY_SORTED_LAUNCH(true, 0);
   else ANNETY_SORTED_LAUNCH(false, 0);
 #else

@@ -247,7 +247,7 @@ class Workload:
         from annety_amd import _lib
 
         self._fixed = _lib.get().annety_crc32_batch_fixed
-        self._data_ptr = self.data.data_ptr()
+        self._data_ptr = self.data.data_ptr() if args.config != "frames" else self.src.data_ptr()
 
     def _init_frames(self, args, dev, rank, gen):
         """--config frames: n payloads (16 B-1 KiB uniform, or all 408 B) packed in a source buffer, and the

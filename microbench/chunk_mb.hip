@@ -25,7 +25,7 @@ constexpr int kBlock = 512, kBlocks = 256, kWaves = kBlocks * kBlock / 64;
 constexpr size_t kBytes = 1ull << 30;
 
 // C = chunk KiB per group per step (1, 2, 4, 8); WINDOW = config-1 pattern
-template <int C, bool WINDOW, int FAKE>
+template <int C, bool WINDOW, int FAKE, int MIS = 0>
 __global__ __launch_bounds__(kBlock) void k_chunk(const uint8_t* __restrict__ base, const uint32_t* __restrict__ perm,
                                                   uint32_t* __restrict__ out) {
   const uint32_t l = threadIdx.x & 63;
@@ -46,7 +46,9 @@ __global__ __launch_bounds__(kBlock) void k_chunk(const uint8_t* __restrict__ ba
       } else {
         const int g = i / C, piece = i % C;  // load i: piece `piece` of group g's chunk
         const size_t stream = (size_t)perm[w * NG + g];
-        a = stream * kStreamBytes + (size_t)s * 1024 * C + 1024 * piece;
+        // MIS: every stream starts MIS bytes past its 64 KiB-aligned place (the sorted path's rounds start at any
+        // 128-byte line); the buffer has 4 KiB of slack past kBytes for the last stream's tail
+        a = stream * kStreamBytes + MIS + (size_t)s * 1024 * C + 1024 * piece;
       }
       v[i] = __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(base + a + lane_off));
     }
@@ -60,29 +62,29 @@ __global__ __launch_bounds__(kBlock) void k_chunk(const uint8_t* __restrict__ ba
   out[blockIdx.x * kBlock + threadIdx.x] = acc;
 }
 
-template <int C, bool WINDOW, int FAKE>
+template <int C, bool WINDOW, int FAKE, int MIS = 0>
 int run(const uint8_t* d, const uint32_t* perm, uint32_t* out, const char* name) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  for (int i = 0; i < 5; i++) k_chunk<C, WINDOW, FAKE><<<kBlocks, kBlock>>>(d, perm, out);
+  for (int i = 0; i < 5; i++) k_chunk<C, WINDOW, FAKE, MIS><<<kBlocks, kBlock>>>(d, perm, out);
   CK(hipEventRecord(e0));
   const int reps = 50;
-  for (int i = 0; i < reps; i++) k_chunk<C, WINDOW, FAKE><<<kBlocks, kBlock>>>(d, perm, out);
+  for (int i = 0; i < reps; i++) k_chunk<C, WINDOW, FAKE, MIS><<<kBlocks, kBlock>>>(d, perm, out);
   CK(hipEventRecord(e1));
   CK(hipEventSynchronize(e1));
   float ms = 0;
   CK(hipEventElapsedTime(&ms, e0, e1));
   ms /= reps;
-  printf("%-10s C=%d fake=%3d  %.4f ms  %.1f GB/s\n", name, C, FAKE, ms, kBytes / (ms * 1e-3) / 1e9);
+  printf("%-10s C=%d fake=%3d mis=%3d  %.4f ms  %.1f GB/s\n", name, C, FAKE, MIS, ms, kBytes / (ms * 1e-3) / 1e9);
   return 0;
 }
 
 int main() {
   uint8_t* d = nullptr;
   uint32_t *perm = nullptr, *out = nullptr;
-  CK(hipMalloc(&d, kBytes));
-  CK(hipMemset(d, 1, kBytes));
+  CK(hipMalloc(&d, kBytes + 4096));  // slack: a misaligned stream's last piece reads up to 1 KiB past kBytes
+  CK(hipMemset(d, 1, kBytes + 4096));
   CK(hipMalloc(&out, kBlocks * kBlock * 4));
   const size_t maxs = (size_t)kWaves * 8;
   CK(hipMalloc(&perm, maxs * 4));
@@ -102,6 +104,10 @@ int main() {
       if (c == 1) {
         run<1, false, 0>(d, perm, out, "streams");
         run<1, false, 200>(d, perm, out, "streams");
+        run<1, false, 0, 128>(d, perm, out, "streams");
+        run<1, false, 0, 384>(d, perm, out, "streams");
+        run<1, false, 0, 640>(d, perm, out, "streams");
+        run<1, false, 0, 512>(d, perm, out, "streams");
       } else if (c == 2) {
         run<2, false, 0>(d, perm, out, "streams");
         run<2, false, 200>(d, perm, out, "streams");
