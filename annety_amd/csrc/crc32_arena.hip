@@ -543,9 +543,14 @@ __device__ __forceinline__ void block_reduce4(uint64_t lo, uint64_t hi, uint64_t
 }
 
 // Bucket of a non-empty payload at absolute address a: 1023 - its 128-byte line count (longest first).
+// key: the payload's rounds in the sorted path (crc32_kernels.hip var_class_w8), R = ceil(lines / 8), descending
+// (payloads of equal R run in lockstep; up to 8184 lines sort exactly, longer ones share bucket 0). Keying on R
+// rather than on lines gives config 3 about 65 distinct buckets instead of about 520, so step 1 issues that many
+// fewer global atomics per block.
 __device__ __forceinline__ uint32_t bucket_of(uint64_t a, uint32_t len) {
   const uint32_t nl = (uint32_t)(((a + len - 1) >> 7) - (a >> 7) + 1);
-  return (kBucketCount - 1) - (nl < kBucketCount - 1 ? nl : kBucketCount - 1);
+  const uint32_t r = (nl + 7) >> 3;
+  return (kBucketCount - 1) - (r < kBucketCount - 1 ? r : kBucketCount - 1);
 }
 
 // COUNT: step 1 of the counting sort (crc32_kernels.h BucketArgs) beside the extent.
@@ -614,13 +619,10 @@ __global__ __launch_bounds__(kBucketThreads) void crc32_bucket_place(const uint6
   basep[t] = start + mine;
   if (blockIdx.x == 0) {
     bk.cursor_next[t] = 0u;
-    // classes by line count (bucket = 1023 - lines): >= 9 lines (crc32_kernels.hip var_class_w8), an empty
-    // middle range, <= 8 lines (var_class_s8)
-    constexpr uint32_t b16 = kBucketCount - 9, b4 = kBucketCount - 9;  // bucket 1015 = 8 lines
+    // one class: every non-empty payload (crc32_kernels.hip var_class_w8); ranges[2..5] empty
     if (t == 0) bk.ranges[0] = 0u;
-    if (t == b16) bk.ranges[1] = bk.ranges[2] = start;
-    if (t == b4) bk.ranges[3] = bk.ranges[4] = start;
-    if (t == kBucketCount - 1) bk.ranges[5] = start + tot;
+    if (t == kBucketCount - 1)
+      bk.ranges[1] = bk.ranges[2] = bk.ranges[3] = bk.ranges[4] = bk.ranges[5] = start + tot;
     if (record && w == 0) {
       uint64_t lo, hi, sum, bad;
       extent_of(ws, parts, lo, hi, sum, bad);

@@ -83,7 +83,7 @@ struct HostImages {
   std::vector<uint32_t> unshift; // 24 maps x 128 words (U_lo[0..15], U_hi[0..7])
   std::vector<uint32_t> sb;      // arena superblock join: (k, v, g) = shift_{(7-g)*1024}(v << 4k); byte map
   std::vector<uint32_t> stitch;  // arena stitch: segment maps F/G/UL/UB, unshift, shift_32 (crc32_math.h)
-  std::vector<uint32_t> w8;      // sorted path, >= 9-line class: join, byte maps, unshift (crc32_math.h kLdsW8*)
+  std::vector<uint32_t> w8;      // sorted path (var_class_w8): join, byte maps, unshift (crc32_math.h kLdsW8*)
 };
 
 // Apply matrix m to (v << 4k) for every nibble value: the 16-entry table of one nibble position.
@@ -228,6 +228,8 @@ const HostImages& host_images() {
           for (uint32_t e = 0; e < 256; e++) bm[kk * 256 + e] = gf2_apply(sm, e << (8 * kk));
       }
       std::memcpy(m + (kLdsW8UnshiftOff - kLdsCommonBytes) / 4, img.unshift.data(), img.unshift.size() * 4);
+      for (uint32_t lead = 0; lead < 128; lead++)
+        m[(kLdsW8InitOff - kLdsCommonBytes) / 4 + lead] = gf2_apply(shift_matrix(128 - lead), kInit);
     }
   });
   return img;
@@ -531,7 +533,7 @@ int scratch_done(DeviceCtx& c, ScratchSlot* slot) {
   return c.slots.done(ops, slot);
 }
 
-// Variable batch: counting sort by line count on the device (no host round trip; two launches,
+// Variable batch: counting sort by rounds (ceil(lines / 8)) on the device (no host round trip; two launches,
 // crc32_kernels.h BucketArgs), then one launch per length class with its own lane-group width. Scratch:
 // the stream's slot (scratch_slot): the bucket cursors in the extent area, rows + ranges + descriptors
 // after it.
@@ -588,12 +590,11 @@ int run_var_sorted_in(DeviceCtx& c, ScratchSlot* slot, const void* d_base, size_
     a.img_unshift = c.d_unshift;
     a.out = d_out;
     a.max_blocks = grid_cus(c);
-    const hipError_t e = launch_var_sorted(a, c.d_w8, group_image(c, 8), stream);
+    const hipError_t e = launch_var_sorted(a, c.d_w8, stream);
     return e == hipSuccess ? ANNETY_CRC_OK : hip_fail(e);
   }
-  const uint32_t groups[3] = {32, 16, 4};  // (A/B builds) lanes per payload of the >= 9-line / empty / small class
-  for (int k = 0; k < 3 && rc == ANNETY_CRC_OK; k++)
-    rc = run_var(c, d_base, n, 0, 0, groups[k], bk.desc, bk.ranges + 2 * k, d_out, stream, update);
+  // (A/B builds) the per-task var kernel over the sorted list, 32 lanes per payload
+  rc = run_var(c, d_base, n, 0, 0, 32, bk.desc, bk.ranges, d_out, stream, update);
   return rc;
 }
 

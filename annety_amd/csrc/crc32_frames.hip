@@ -34,7 +34,7 @@ __global__ __launch_bounds__(256) void lhc_compare_kernel(const uint8_t* __restr
 // once. One lane group of 8 per frame, frames i = group, group + groups, ... Rounds of 8 end-aligned 128-byte
 // lines (lane j holds line 8 r + j - vlead of the payload, the lanes before line 0 re-read it), per-line loads
 // plus the first dword of the next line. From the same registers:
-//   * the CRC, as var_class_s8 (bytes outside the payload masked, the init as the register shift_{128-lead}(init)
+//   * the CRC, as the sorted path's one-round payloads (bytes outside the payload masked, the init as the register shift_{128-lead}(init)
 //     of line 0, rounds chained through shift_{7*128}, the join and the inverse shift of the last line's
 //     overhang);
 //   * the copy: every destination-aligned dword whose four bytes are payload bytes is stored by the lane holding

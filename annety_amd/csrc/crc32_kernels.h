@@ -63,10 +63,9 @@ struct VarLaunch {
 };
 
 hipError_t launch_var(const VarLaunch& a, hipStream_t stream);
-// The sorted path's length classes in one launch (a.range = their 6 bounds: >= 9 lines, empty, <= 8 lines);
-// img_w8 = the w8 image (kW8ImgBytes, crc32_math.h), img_g8 = the G = 8 group part; a.group and a.img_group are
-// ignored.
-hipError_t launch_var_sorted(const VarLaunch& a, const void* img_w8, const void* img_g8, hipStream_t stream);
+// The sorted path in one launch (a.range[0..1] = the sorted list's bounds in a.desc); img_w8 = the w8 image
+// (kW8ImgBytes, crc32_math.h); a.group, a.img_group and a.img_unshift are ignored.
+hipError_t launch_var_sorted(const VarLaunch& a, const void* img_w8, hipStream_t stream);
 
 // Long payloads cut into end-aligned segments (crc32_kernels.hip): descriptors for the variable kernel,
 // then the combine fold with powers[(m-1)*32 + bit] = shift_{m*seg}(1 << bit), m = 1..S-1.
@@ -123,11 +122,11 @@ struct ArenaLaunch {
   uint64_t record_seq;
 };
 
-// Counting sort of a variable batch by 128-byte line count, longest first, for the sorted path: two
-// launches, no host round trip and no memset per call.
-//  1. launch_extent with `bk`: besides the extent partials, each block histograms its payloads by line count
-//     in LDS and claims its slots in every bucket it uses with one agent-scope atomic add on that bucket's
-//     cursor (rows[b][i] = the value returned = block b's first slot inside bucket i, in arrival order),
+// Counting sort of a variable batch by rounds (ceil(128-byte lines / 8)), longest first, for the sorted path:
+// two launches, no host round trip and no memset per call.
+//  1. launch_extent with `bk`: besides the extent partials, each block histograms its payloads by that key in
+//     LDS and claims its slots in every bucket it uses with one agent-scope atomic add on that bucket's cursor
+//     (rows[b][i] = the value returned = block b's first slot inside bucket i, in arrival order),
 //     and writes out[p] = 0 for zero-length payloads (out null in update mode: their registers stay).
 //  2. launch_bucket_place: every block scans the 1024 cursor totals into bucket bases, ranks its payloads
 //     inside its slots with LDS atomics and writes desc[] (16 B per non-empty payload); block 0 writes the
@@ -146,7 +145,7 @@ struct BucketArgs {
   uint32_t* rows;         // bucket_grid(n) * kBucketCount words
   uint32_t* cursor;       // this call's set (zero on entry)
   uint32_t* cursor_next;  // the other set: zeroed by launch_bucket_place
-  uint32_t* ranges;       // kRangeWords: {begin, end} of the classes (>= 9 lines, empty, <= 8 lines) in desc
+  uint32_t* ranges;       // kRangeWords: [0, 1] = {begin, end} of the sorted list in desc, [2..5] empty
   void* desc;             // uint4 {addr lo, addr hi, len, index} per non-empty payload
   uint32_t* out;          // zero-length digests; null in update mode
 };

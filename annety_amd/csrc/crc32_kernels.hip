@@ -380,8 +380,7 @@ __global__ __launch_bounds__(BLK) void crc32_fixed32_nt_kernel(const uint8_t* __
 // Lines are assigned end-aligned over rounds of G lanes, exactly like the fixed kernel, and the
 // (task, round) steps are double-buffered across task boundaries.
 // `order`/`range` (optional) select the tasks: order[range[0] .. range[1]) are payload indices sorted
-// by line count (crc32_bucket_place, crc32_arena.hip), so the payloads of a wave finish together and each length
-// class runs with its own G. Zero-length payloads never reach this kernel (the bucket pass writes 0).
+// by rounds of 8 lines (crc32_bucket_place, crc32_arena.hip), so the payloads of a wave finish together. Zero-length payloads never reach this kernel (the bucket pass writes 0).
 struct VarTask {
   uint64_t line0;    // absolute index of the payload's first 128-byte line
   uint32_t nlines, rounds, vlead, lead, tailend, len, p;
@@ -623,13 +622,13 @@ __global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __rest
 }
 
 // ---------------------------------------------------------------------------------------------
-// The length-sorted path's class of payloads of >= 9 lines (round 5): lane groups of G = 8 on
-// coalesced nontemporal 1 KiB loads, with the steady-state round of crc32_onekib_nt_kernel and no per-lane
-// masks, clamps or address arithmetic in it.
+// The length-sorted path (round 5): lane groups of G = 8 on coalesced nontemporal 1 KiB loads,
+// with the steady-state round of crc32_onekib_nt_kernel and no per-lane masks or address arithmetic in it.
 //
 // A payload of nl lines (absolute 128-byte lines L0..L1) is cut into R = (nl - h) / 8 + 1 rounds:
 //   round 0 ("head"): lines [0, 8) read start-aligned, of which the first h = ((nl - 1) mod 8) + 1 are the
-//            payload's (bytes before the payload start masked, lines >= h zeroed), then each lane's register is
+//            payload's (bytes before the payload start masked, lines >= h zeroed; a payload of <= 8 lines, R = 1,
+//            re-reads its last line in their place and ends in this round), then each lane's register is
 //            moved (8 - h) lanes up inside its group (ds_bpermute), so that the group holds the head end-aligned,
 //            and the init (or the caller's register) enters as the register shift_{128-lead}(init) of line 0;
 //   rounds 1 .. R-1 ("body"): the 1 KiB pieces [h + 8 (r - 1), h + 8 r): whole lines, except that the last
@@ -656,7 +655,7 @@ struct W8Task {
 __device__ __forceinline__ W8Task decode_w8(uint4 d, bool valid) {
   W8Task k;
   const uint64_t a = ((uint64_t)d.y << 32) | d.x;
-  const uint64_t e = a + d.z;  // length >= 9 lines' worth, so > 0
+  const uint64_t e = a + d.z;  // d.z > 0
   const uint64_t L0 = a >> 7;
   const uint32_t nl = (uint32_t)(((e - 1) >> 7) - L0 + 1);
   k.a0 = L0 << 7;
@@ -683,14 +682,12 @@ __device__ __forceinline__ uint32_t w8_join(uint32_t s, const uint32_t* lds, uin
   return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6] ^ r[7]);
 }
 
-//   STAGE: 1 = stage the whole image (also for a block without work of this class), 0 = only the w8 part (the
-//   common part is in place).
 //   PROBE (A/B builds only, microbench/sorted_probe.py; product = 0): bit 0 = every step takes the unmasked
 //   branch, bit 1 = no fold (the data are xored into the register), bit 2 = loads from config 1's window (wave w,
 //   step s: 8 KiB at (s W + w) 8 KiB) instead of the tasks' rounds, bit 3 = the same window loaded with config 1's
 //   scalar base and immediate offsets - wrong digests, used to measure what the masked rounds, the fold, the
 //   access pattern and the per-group addressing cost.
-template <bool UPD, int STAGE, int PROBE = 0>
+template <bool UPD, int PROBE = 0>
 __device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restrict__ base,
                                              const uint4* __restrict__ desc, const uint32_t* __restrict__ range,
                                              const uint4* __restrict__ img_slice, const uint4* __restrict__ img_w8,
@@ -698,8 +695,8 @@ __device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restr
   constexpr int G = 8;
   const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
   const uint32_t l = threadIdx.x & 63, l3 = (l >> 3) & 1, j = l & 7;
-  const size_t gid = group_id<kBlock, G, kVwg>();
-  const size_t ngroups = ((size_t)gridDim.x * kBlock) / G;
+  const size_t gid = group_id<kW8Block, G, kVwg>();
+  const size_t ngroups = ((size_t)gridDim.x * kW8Block) / G;
   const size_t t_begin = range[0], t_end = range[1];
   LaneCtx k;
   k.L0 = (threadIdx.x & 31) << 3;
@@ -710,8 +707,8 @@ __device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restr
   auto raw = [&](size_t t) { return raw_task<true>(t, t_end, base, desc, 0, 0); };
   // Load i reads the round of lane group m(i) = (i >> 2) + 2 (i & 1) + 4 ((i >> 1) & 1), so that after
   // transpose_blocks lane l holds half l3 of line j of the even group of its pair (l >> 3 & ~1) in v[0..3] and of
-  // the odd one in v[4..7] (crc32_onekib_nt_kernel's layout). Invalid groups decode the last task of the class
-  // (raw_task clamps), so every address is inside a payload of >= 9 lines.
+  // the odd one in v[4..7] (crc32_onekib_nt_kernel's layout). Invalid groups decode the last task of the list
+  // (raw_task clamps), so every address is inside a payload's lines.
   uint32_t wstep = 0;  // steps so far (PROBE bits 2, 3)
   auto load = [&](const W8Task& tk, uint32_t r, uint4 (&v)[8]) __attribute__((always_inline)) {
     uint64_t ad = tk.a0 + (r == 0 ? 0ull : (uint64_t)tk.h * 128u + (uint64_t)(r - 1) * 1024u);
@@ -729,13 +726,18 @@ __device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restr
       return;
     }
     const uint32_t lo = (uint32_t)ad, hi = (uint32_t)(ad >> 32);
+    // a payload of <= 8 lines is one round (R = 1) whose lines [h, 8) lie past its end: those lanes re-read its
+    // last line (masked to zero in compute), so no load leaves the payload's lines
+    const uint32_t cl = r == 0 && tk.R == 1 ? tk.h - 1 : 7u;
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       const int src = 8 * ((i >> 2) + 2 * (i & 1) + 4 * ((i >> 1) & 1));
       const uint64_t g = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, src) << 32) |
                          (uint32_t)__builtin_amdgcn_readlane((int)lo, src);
+      const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cl, src);
       const uint8_t* gb = base + (g - b0);
-      const v4u32 x = __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(gb + voff));
+      const v4u32 x =
+          __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(gb + ((min(j, c) << 7) | (voff & 127u))));
       v[i] = make_uint4(x.x, x.y, x.z, x.w);
     }
   };
@@ -743,42 +745,64 @@ __device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restr
   // Sets: block b owns the sets k NB + b (k even) and k NB + NB - 1 - b (k odd), NB = the grid's blocks (snake
   // order over the sorted list, so every block gets an even share of long and short sets); its 8 waves take them
   // in list order, wave w the w-th first, every later one from a counter in LDS when the wave's set is 3 steps from
-  // its end (the descriptors come from HBM in the meantime): longest first, each to the wave that frees up first.
-  __shared__ uint32_t sets_taken;
-  const uint32_t nb = gridDim.x, bb = blockIdx.x, m = l >> 3;
+  // its end, or a second one ahead while its sets last at most 2 steps: longest first, each to the wave that frees
+  // up first (with the shortest interleaved, below). A claim's descriptors load into a register (one per step parity) and land in the wave's ring in LDS
+  // at the next step, before its switch reads them: a register copy of a load in flight would wait for it.
+  const uint32_t nb = gridDim.x, bb = blockIdx.x, m = l >> 3, wl = threadIdx.x >> 6;
   const uint32_t nsets = (uint32_t)((t_end - t_begin + 7) / 8);
   auto set_of = [&](uint32_t kk) {
     const uint64_t g = (uint64_t)kk * nb + ((kk & 1u) ? nb - 1 - bb : bb);
     return g < nsets ? (uint32_t)g : nsets;  // nsets: no set (every task_of >= t_end)
   };
   auto task_of = [&](uint32_t set) { return t_begin + 8 * (size_t)set + m; };
-  uint32_t S0 = set_of(threadIdx.x >> 6);  // the set being loaded; S1, the next one (descriptors in rn), below
-  if (!__syncthreads_or(task_of(S0) < t_end)) {  // the block has no task of this class
-    if constexpr (STAGE == 1) {
-      load_image<kLdsW8ImageBytes, kBlock, kLdsCommonBytes>(lds4, img_slice, nullptr, img_w8);
-      __syncthreads();
-    }
-    return;
-  }
-  // Pipeline: the load side holds the task whose round rL it loads this step (dL); rn is the raw descriptor of
-  // this group's task in the next set, fetched every other step from the same address (a claim comes at least
-  // two steps before its switch), so a switch never waits on HBM. The compute side (dC, rC) is the load side one
-  // step later.
+  uint32_t S0 = set_of(wl);  // the set being loaded
+  if (!__syncthreads_or(task_of(S0) < t_end)) return;  // the block has no task
+  uint4* const ring = lds4 + kLdsW8RingOff / 16 + wl * 4 * 8;  // [slot][group], 4 slots
+  uint32_t* const ring_set = reinterpret_cast<uint32_t*>(lds4) + kLdsW8RingSetOff / 4 + wl * 4;
+  uint64_t* const sets_taken = reinterpret_cast<uint64_t*>(lds4) + kLdsW8CounterOff / 8;
+  // the block's sets: k NB + (b or NB - 1 - b) < nsets for k < nk
+  const uint32_t full = nsets / nb, rem = nsets % nb;
+  const uint32_t nk = full + (((full & 1u) ? nb - 1 - bb : bb) < rem ? 1u : 0u);
+  // Pipeline: the load side holds the task whose round rL it loads this step (dL); the compute side (dC, rC) is
+  // the load side one step later. Claimed sets [head, tail) wait in the ring (slot = index mod 4).
   W8Task dL = decode_w8(raw(task_of(S0)), task_of(S0) < t_end);
   if constexpr (UPD) dL.state = dL.valid ? out[dL.p] : 0u;
   uint4 A[8], B[8];
   load(dL, 0, A);
-  uint32_t S1 = nsets;  // not claimed yet
-  bool claimed = false;
-  uint4 rn = raw(task_of(S1));
   W8Task dC = dL;
-  uint32_t rC = 0, rL = 1;
-  if constexpr (STAGE == 0)
-    load_image<kLdsW8ImageBytes, kBlock, kLdsCommonBytes, kLdsCommonBytes>(lds4, img_slice, nullptr, img_w8);
-  else
-    load_image<kLdsW8ImageBytes, kBlock, kLdsCommonBytes>(lds4, img_slice, nullptr, img_w8);
-  if (threadIdx.x == 0) sets_taken = kBlock / 64;
+  uint32_t rC = 0, rL = 1, head = 0, tail = 0;
+  uint4 inA = make_uint4(0, 0, 0, 0), inB = inA;  // a claim's descriptors in flight, by step parity
+  uint32_t setA = 0, setB = 0;
+  bool pendA = false, pendB = false;
+  load_image<kLdsW8ImageBytes, kW8Block, kLdsCommonBytes>(lds4, img_slice, nullptr, img_w8);
+  if (threadIdx.x == 0) *sets_taken = kW8Block / 64;  // front: the waves' first sets; back: none
   __syncthreads();
+
+  // claim rule (wave-uniform): no set queued and S0 within 3 steps of its end, or fewer than 2 queued while S0
+  // lasts at most 2 steps
+  // The claims alternate between the front of the block's list and its back (the shortest sets, mostly one masked
+  // round each), so that the masked rounds' arithmetic overlaps other waves' streaming instead of filling the
+  // launch's tail. One 64-bit counter holds both ends' counts, so no set is taken twice.
+  bool back = true;
+  auto maybe_claim = [&](uint4& in, uint32_t& set, bool& pend) __attribute__((always_inline)) {
+    const uint32_t q = tail - head;
+    const bool near = __builtin_amdgcn_ballot_w64(rL + 3 < dL.R) == 0;
+    const bool shrt = __builtin_amdgcn_ballot_w64(dL.R > 2) == 0;
+    if ((near && q == 0) || (shrt && q < 2)) {
+      uint64_t old = 0;
+      if (l == 0)
+        old = __hip_atomic_fetch_add(sets_taken, back ? (1ull << 32) : 1ull, __ATOMIC_RELAXED,
+                                     __HIP_MEMORY_SCOPE_WORKGROUP);
+      const uint32_t f = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)old),
+                     bk = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(old >> 32));
+      set = f + bk < nk ? set_of(back ? nk - 1 - bk : f) : nsets;
+      back = !back;
+      in = raw(task_of(set));
+      pend = true;
+      tail++;
+    }
+  };
+  maybe_claim(inB, setB, pendB);  // (a first set of <= 4 rounds: its successor is due at once)
 
   uint32_t s = 0;
   auto fold = [&](uint4 (&v)[8]) __attribute__((always_inline)) {
@@ -814,7 +838,9 @@ __device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restr
     // and 1 - l3 (sent to lane ^ 8, whose v holds this group's half 1 - l3 ... = the partner's own half).
     const bool head = cur.valid && r_c == 0, last = cur.valid && r_c + 1 == cur.R;
     const int32_t line_lo = head && j == 0 ? (int32_t)cur.lead : 0;
-    const int32_t line_hi = !cur.valid || (head && j >= cur.h) ? 0 : (last && j == 7 ? (int32_t)cur.te : 128);
+    // (the last line: line 7 of a last round, line h - 1 of a one-round payload's head round)
+    const int32_t line_hi =
+        !cur.valid || (head && j >= cur.h) ? 0 : (last && j == (head ? cur.h - 1 : 7u) ? (int32_t)cur.te : 128);
     const int32_t lo_own = min(max(line_lo - 64 * (int32_t)l3, 0), 64), hi_own = min(max(line_hi - 64 * (int32_t)l3, 0), 64);
     const int32_t lo_oth = min(max(line_lo - 64 * (int32_t)(l3 ^ 1), 0), 64),
                   hi_oth = min(max(line_hi - 64 * (int32_t)(l3 ^ 1), 0), 64);
@@ -843,10 +869,12 @@ __device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restr
       const uint32_t moved = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * src, (int)s);
       s = head ? (from ? moved : 0u) : s;
       if (head && j == up) {
-        uint32_t x = UPD ? cur.state : kInit;
-        x = w8_unshift(x, cur.lead, lds);                                            // shift_{-lead}
-        x = byte_map64(byte_map64(x, lds, kLdsW8HalfOff), lds, kLdsW8HalfOff);       // shift_128
-        s ^= x;
+        if constexpr (UPD) {
+          uint32_t x = w8_unshift(cur.state, cur.lead, lds);                       // shift_{-lead}
+          s ^= byte_map64(byte_map64(x, lds, kLdsW8HalfOff), lds, kLdsW8HalfOff);  // shift_128
+        } else {
+          s ^= lds[kLdsW8InitOff / 4 + cur.lead];  // shift_{128-lead}(kInit)
+        }
       }
     }
     if (__builtin_amdgcn_ballot_w64(last) != 0) {
@@ -860,23 +888,23 @@ __device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restr
     }
   };
 
-  auto step = [&](uint4 (&cur_buf)[8], uint4 (&nxt_buf)[8], bool fetch) __attribute__((always_inline)) {
-    if (__builtin_amdgcn_ballot_w64(rL + 3 < dL.R) == 0) {  // every group of the wave is within 3 steps of its end
-      if (!claimed) {  // (wave-uniform) the next set from the block's counter
-        uint32_t kk = 0;
-        if (l == 0) kk = __hip_atomic_fetch_add(&sets_taken, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        S1 = set_of((uint32_t)__builtin_amdgcn_readfirstlane((int)kk));
-        claimed = fetch = true;
-      }
-      if (__builtin_amdgcn_ballot_w64(rL < dL.R) == 0) {  // every group is done with S0: switch
-        S0 = S1;
-        claimed = false;
-        dL = decode_w8(rn, task_of(S0) < t_end);
-        if constexpr (UPD) dL.state = dL.valid ? out[dL.p] : 0u;
-        rL = 0;
-      }
+  auto step = [&](uint4 (&cur_buf)[8], uint4 (&nxt_buf)[8], uint4& in_new, uint32_t& set_new, bool& pend_new,
+                  const uint4& in_old, uint32_t set_old, bool& pend_old) __attribute__((always_inline)) {
+    if (pend_old) {  // the previous step's claim (index tail - 1) lands; its load preceded that step's data loads
+      const uint32_t slot = (tail - 1) & 3u;
+      if (j == 0) ring[slot * 8 + m] = in_old;
+      if (l == 0) ring_set[slot] = set_old;
+      pend_old = false;
     }
-    if (fetch) rn = raw(task_of(S1));
+    if (__builtin_amdgcn_ballot_w64(rL < dL.R) == 0) {  // every group is done with S0: the queue's head
+      const uint32_t slot = head & 3u;
+      head++;
+      S0 = ring_set[slot];
+      dL = decode_w8(ring[slot * 8 + m], task_of(S0) < t_end);
+      if constexpr (UPD) dL.state = dL.valid ? out[dL.p] : 0u;
+      rL = 0;
+    }
+    maybe_claim(in_new, set_new, pend_new);
     ANNETY_PRIO_HI();
     load(dL, dL.valid && rL < dL.R ? rL : 0u, nxt_buf);
     __builtin_amdgcn_sched_barrier(0);
@@ -890,151 +918,24 @@ __device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restr
   // wave-uniform loop: the loads and the cross-lane steps need every group (a finished group reads a round of
   // the class's last payload and stores nothing)
   while (__builtin_amdgcn_ballot_w64(dC.valid) != 0) {
-    step(A, B, true);
-    step(B, A, false);
+    step(A, B, inA, setA, pendA, inB, setB, pendB);
+    step(B, A, inB, setB, pendB, inA, setA, pendA);
   }
 }
 
-// The length-sorted path's class of payloads of <= 8 lines (round 5): one task = one payload = one round of a
-// lane group of 8 lanes. Lane j folds line j - (8 - nl) of the payload (end-aligned: the lanes before line 0
-// re-read line 0 and zero it) from register 0 with per-line loads; bytes before the payload start and past its
-// end are masked, the init (or the caller's register) enters as the register shift_{128-lead}(init) of line 0
-// (so 1-3 byte payloads and an init that spills into the second line need no case of their own), and the
-// group's join leaves the register at the last line's end, from which the inverse shift of the overhang gives
-// the payload's. Latency-bound (a descriptor, then at most 1 KiB of lines, per task): descriptors are fetched
-// two tasks ahead of their lines and the lines one task ahead of their fold, every load unconditional (a
-// finished group re-reads the class's last payload and stores nothing).
-//   STAGE as var_class: 1 = the whole var image with the G = 8 group part, 3 = the group part and the inverse
-//   shifts only (the common part is in place).
-struct S8Task {
-  uint64_t L0;  // the payload's first line (absolute 128-byte line index)
-  uint32_t nl, lead, te, p;
-  bool valid;
-};
-__device__ __forceinline__ S8Task decode_s8(uint4 d, bool valid) {
-  S8Task k;
-  const uint64_t a = ((uint64_t)d.y << 32) | d.x;
-  const uint64_t e = a + d.z;  // d.z > 0
-  k.L0 = a >> 7;
-  k.nl = (uint32_t)(((e - 1) >> 7) - k.L0 + 1);
-  k.lead = (uint32_t)(a & 127);
-  k.te = (uint32_t)(((e - 1) & 127) + 1);
-  k.p = d.w;
-  k.valid = valid;
-  return k;
-}
-template <bool UPD, int STAGE>
-__device__ __forceinline__ void var_class_s8(uint4* lds4, const uint8_t* __restrict__ base,
-                                             const uint4* __restrict__ desc, const uint32_t* __restrict__ range,
-                                             const uint4* __restrict__ img_slice, const uint4* __restrict__ img_g8,
-                                             const uint4* __restrict__ img_unshift, uint32_t* __restrict__ out) {
-  constexpr int G = 8;
-  const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
-  const uint32_t j = threadIdx.x & 7;
-  const size_t gid = group_id<kBlock, G, kVwg>();
-  const size_t ngroups = ((size_t)gridDim.x * kBlock) / G;
-  const size_t t_begin = range[0], t_end = range[1];
-  LaneCtx k;
-  k.L0 = (threadIdx.x & 31) << 3;
-  k.L1 = k.L0 | (1u << 16);
-  k.slot4 = (threadIdx.x & 31) << 2;                      // join slot: shift_{(7-j)*128}
-  const uint32_t slot128 = ((threadIdx.x & 24) | 6) << 2;  // this replica row's slot j = 6: shift_128
-  auto raw = [&](size_t t) { return raw_task<true>(t, t_end, base, desc, 0, 0); };
-  auto load = [&](const S8Task& tk, uint4 (&v)[8], uint32_t& st) __attribute__((always_inline)) {
-    const int32_t li = (int32_t)j - (int32_t)(8 - tk.nl);
-    const uint64_t src = (tk.L0 + (uint64_t)(li > 0 ? li : 0)) << 7;
-#pragma unroll
-    for (int i = 0; i < 8; i++) v[i] = gload16(src + 16 * i);
-    if constexpr (UPD) st = out[tk.p];
-  };
-
-  size_t t = t_begin + gid;  // the task computed this step
-  if (!__syncthreads_or(t < t_end)) {
-    if constexpr (STAGE == 1) {
-      load_image<kLdsVarImageBytes>(lds4, img_slice, img_g8, img_unshift);
-      __syncthreads();
-    }
-    return;
-  }
-  S8Task cur = decode_s8(raw(t), t < t_end);
-  uint4 A[8], B[8];
-  uint32_t stA = 0, stB = 0;
-  load(cur, A, stA);
-  uint4 d1 = raw(t + ngroups), d2 = raw(t + 2 * ngroups);  // the next two tasks' descriptors
-  if constexpr (STAGE == 3)
-    load_image<kLdsVarImageBytes, kBlock, kLdsImageBytes, kLdsCommonBytes>(lds4, img_slice, img_g8, img_unshift);
-  else
-    load_image<kLdsVarImageBytes>(lds4, img_slice, img_g8, img_unshift);
-  __syncthreads();
-
-  auto compute = [&](uint4 (&v)[8], const S8Task& tk, uint32_t st) __attribute__((always_inline)) {
-    const int32_t li = (int32_t)j - (int32_t)(8 - tk.nl);
-    const int32_t lo = li == 0 ? (int32_t)tk.lead : 0;
-    const int32_t hi = li < 0 ? 0 : (li == (int32_t)tk.nl - 1 ? (int32_t)tk.te : 128);
-    mask_line<8>(v, lo * 8, hi * 8);
-    uint32_t s = absorb_line(0u, v, k, lds);
-    if (li == 0) {  // the init as the register at the payload start: shift_{128-lead}(init) at line 0's end
-      uint32_t x = UPD ? st : kInit;
-      x = nibble_map_uniform(x, lds, kLdsUnshiftOff + (tk.lead & 15u) * 512);
-      x = nibble_map_uniform(x, lds, kLdsUnshiftOff + 8192 + (tk.lead >> 4) * 512);
-      s ^= nibble_map_lane(x, lds, slot128);
-    }
-    uint32_t r = group_xor_reduce<G>(nibble_map_lane(s, lds, k.slot4));
-    if (tk.valid && j == G - 1) {
-      const uint32_t over = 128 - tk.te;  // the last line's bytes past the payload end (zeroed above)
-      if (over) {
-        r = nibble_map_uniform(r, lds, kLdsUnshiftOff + (over & 15u) * 512);
-        r = nibble_map_uniform(r, lds, kLdsUnshiftOff + 8192 + (over >> 4) * 512);
-      }
-      out[tk.p] = UPD ? r : ~r;
-    }
-  };
-  auto step = [&](uint4 (&cur_buf)[8], uint32_t cur_st, uint4 (&nxt_buf)[8], uint32_t& nxt_st)
-      __attribute__((always_inline)) {
-    const uint4 d3 = raw(t + 3 * ngroups);  // unconditional (clamped past the end)
-    const S8Task nxt = decode_s8(d1, t + ngroups < t_end);
-    load(nxt, nxt_buf, nxt_st);
-    __builtin_amdgcn_sched_barrier(0);
-    compute(cur_buf, cur, cur_st);
-    cur = nxt;
-    t += ngroups;
-    d1 = d2;
-    d2 = d3;
-  };
-  while (__builtin_amdgcn_ballot_w64(cur.valid) != 0) {
-    step(A, stA, B, stB);
-    step(B, stB, A, stA);  // harmless when the group ran out of work on the first half: nothing is stored
-  }
-}
-
-// The sorted path in one launch (ranges[0..5] = the classes' [begin, end) in desc, longest first; crc32_bucket_place):
-// payloads of >= 9 lines (ranges[0..1]) run in var_class_w8, payloads of <= 8 lines (ranges[4..5]) in var_class_s8
-// (per-line loads, one round of 8 lanes each: latency-bound); ranges[2..3] is empty. Odd blocks run the
-// small class first, so that its dependent descriptor -> line -> fold steps overlap other blocks' streaming
-// instead of every block's tail (round 4, profiles/r04/sorted_nt/ab_class_order.log). The classes restage only
-// the part of the LDS image they do not share with the other.
-//   PROBE, classes: A/B builds only (microbench/sorted_probe.py); the product runs PROBE 0 and both classes.
+// The sorted path in one launch: every non-empty payload (desc[ranges[0], ranges[1]), longest first;
+// crc32_bucket_place) in var_class_w8.
+//   PROBE: A/B builds only (microbench/sorted_probe.py); the product runs PROBE 0.
 template <bool UPD, int PROBE = 0>
-__global__ __launch_bounds__(kBlock) void crc32_var_sorted_kernel(const uint8_t* __restrict__ base, size_t n,
+__global__ __launch_bounds__(kW8Block) void crc32_var_sorted_kernel(const uint8_t* __restrict__ base, size_t n,
                                                                   const uint4* __restrict__ desc,
                                                                   const uint32_t* __restrict__ ranges,
                                                                   const uint4* __restrict__ img_slice,
                                                                   const uint4* __restrict__ img_w8,
-                                                                  const uint4* __restrict__ img_g8,
-                                                                  const uint4* __restrict__ img_unshift,
-                                                                  uint32_t* __restrict__ out, uint32_t classes) {
-  __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsVarImageBytes / 16];
-  static_assert(kLdsW8ImageBytes <= kLdsVarImageBytes, "one LDS array serves both classes");
-  const uint32_t* none = ranges + 2;  // the empty middle range: a class switched off (A/B)
-  if (blockIdx.x & 1) {
-    var_class_s8<UPD, 1>(lds4, base, desc, classes & 2 ? ranges + 4 : none, img_slice, img_g8, img_unshift, out);
-    __syncthreads();
-    var_class_w8<UPD, 0, PROBE>(lds4, base, desc, classes & 1 ? ranges : none, img_slice, img_w8, out);
-  } else {
-    var_class_w8<UPD, 1, PROBE>(lds4, base, desc, classes & 1 ? ranges : none, img_slice, img_w8, out);
-    __syncthreads();
-    var_class_s8<UPD, 3>(lds4, base, desc, classes & 2 ? ranges + 4 : none, img_slice, img_g8, img_unshift, out);
-  }
+                                                                  uint32_t* __restrict__ out) {
+  __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsW8TotalBytes / 16];
+  static_assert(kW8Block % 64 == 0 && kW8Block / 64 <= kW8MaxWaves, "the claim rings hold one ring per wave");
+  var_class_w8<UPD, PROBE>(lds4, base, desc, ranges, img_slice, img_w8, out);
 }
 
 // ---- long payloads: segments + CRC combine ----
@@ -1217,26 +1118,21 @@ hipError_t launch_fixed(const FixedLaunch& a, hipStream_t stream) {
   return a.full ? launch_full<true, false>(a, stream) : launch_full<false, false>(a, stream);
 }
 
-hipError_t launch_var_sorted(const VarLaunch& a, const void* img_w8, const void* img_g8, hipStream_t stream) {
+hipError_t launch_var_sorted(const VarLaunch& a, const void* img_w8, hipStream_t stream) {
   const unsigned blocks = (unsigned)std::max<size_t>(1, a.max_blocks);
   note_kernel("crc32_var_sorted_kernel");
 #define ANNETY_SORTED_LAUNCH(UPD, PROBE)                                                                      \
-  hipLaunchKernelGGL((crc32_var_sorted_kernel<UPD, PROBE>), dim3(blocks), dim3(kBlock), 0, stream,            \
+  hipLaunchKernelGGL((crc32_var_sorted_kernel<UPD, PROBE>), dim3(blocks), dim3(kW8Block), 0, stream,            \
                      static_cast<const uint8_t*>(a.base), a.n, static_cast<const uint4*>(a.desc), a.range,      \
-                     static_cast<const uint4*>(a.img_slice), static_cast<const uint4*>(img_w8),                \
-                     static_cast<const uint4*>(img_g8), static_cast<const uint4*>(a.img_unshift), a.out, classes)
+                     static_cast<const uint4*>(a.img_slice), static_cast<const uint4*>(img_w8), a.out)
 #ifdef ANNETY_CRC_AB
-  static const uint32_t classes = (uint32_t)ANNETY_AB_KNOB("ANNETY_CRC_SORTED_CLASSES", 3);
   static const int probe = ANNETY_AB_KNOB("ANNETY_CRC_W8_PROBE", 0);
   if (!a.update && probe == 1) ANNETY_SORTED_LAUNCH(false, 1);
   else if (!a.update && probe == 2) ANNETY_SORTED_LAUNCH(false, 2);
   else if (!a.update && probe == 6) ANNETY_SORTED_LAUNCH(false, 6);
-  else if (!a.update && probe == 10) ANNETY_SORTED_LAUNCH(false, 10);
-  else if (!a.update && probe == 8) ANNETY_SORTED_LAUNCH(false, 8);
   else if (a.update) ANNETY_SORTED_LAUNCH(true, 0);
   else ANNETY_SORTED_LAUNCH(false, 0);
 #else
-  constexpr uint32_t classes = 3;
   if (a.update) ANNETY_SORTED_LAUNCH(true, 0);
   else ANNETY_SORTED_LAUNCH(false, 0);
 #endif

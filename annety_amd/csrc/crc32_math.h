@@ -141,18 +141,29 @@ constexpr uint32_t kLdsQuarterOff = kLdsStitchUnshiftOff + kLdsUnshiftBytes;
 constexpr uint32_t kLdsMidOff = kLdsQuarterOff + 512;
 constexpr uint32_t kMidMaps = 6;  // P(2..7); P(1) = G(8) of the segment set, P(0) = identity
 constexpr uint32_t kLdsStitchImageBytes = kLdsMidOff + kMidMaps * 512;  // 163840: all of the CU's LDS
-// Length-sorted path, class of payloads of >= 9 lines (crc32_kernels.hip var_class_w8): common part, then the
+// Length-sorted path (crc32_kernels.hip var_class_w8): common part, then the
 // device image "w8" (kW8ImgBytes):
 //   [kLdsW8JoinOff, +4 KiB)     lane-position join, unreplicated: (k, v, j) at (k*16 + v)*32 + j*4 =
 //                               shift_{(7-j)*128}(v << 4k) (used once per payload: bank conflicts are harmless)
 //   [kLdsW8HalfOff, +4 KiB)     byte tables of the half-line join shift_64 (crc32_device.h byte_map64)
 //   [kLdsW8RoundOff, +4 KiB)    byte tables of the round advance shift_{7*128}
 //   [kLdsW8UnshiftOff, +12 KiB) U_lo[m] = shift_{-m} (m = 0..15), U_hi[h] = shift_{-16h} (h = 0..7), 512 B each
+//   [kLdsW8InitOff, +512 B)     shift_{128-lead}(kInit), lead = 0..127: the init as a register at line 0's end
 constexpr uint32_t kLdsW8JoinOff = kLdsCommonBytes;
 constexpr uint32_t kLdsW8HalfOff = kLdsW8JoinOff + 4096;
 constexpr uint32_t kLdsW8RoundOff = kLdsW8HalfOff + 4096;
 constexpr uint32_t kLdsW8UnshiftOff = kLdsW8RoundOff + 4096;
-constexpr uint32_t kLdsW8ImageBytes = kLdsW8UnshiftOff + kLdsUnshiftBytes;  // 156160
-constexpr uint32_t kW8ImgBytes = kLdsW8ImageBytes - kLdsCommonBytes;        // 24576
+constexpr uint32_t kLdsW8InitOff = kLdsW8UnshiftOff + kLdsUnshiftBytes;
+constexpr uint32_t kLdsW8ImageBytes = kLdsW8InitOff + 512;            // 156672
+constexpr uint32_t kW8ImgBytes = kLdsW8ImageBytes - kLdsCommonBytes;  // 25088
+// after the image: each wave's ring of 4 claimed sets' descriptors (8 x 16 B a set), their set indices, and the
+// block's set counters (front, back: 2 x 32 bits of one 64-bit word)
+// The sorted kernel's block: 768 threads (12 waves: 3 per SIMD at <= 168 VGPRs) share the one LDS image.
+constexpr int kW8Block = 768;
+constexpr uint32_t kW8MaxWaves = 12;
+constexpr uint32_t kLdsW8RingOff = kLdsW8ImageBytes;
+constexpr uint32_t kLdsW8RingSetOff = kLdsW8RingOff + kW8MaxWaves * 4 * 128;
+constexpr uint32_t kLdsW8CounterOff = kLdsW8RingSetOff + kW8MaxWaves * 4 * 4;
+constexpr uint32_t kLdsW8TotalBytes = kLdsW8CounterOff + 16;  // 163024 <= 163840
 
 }  // namespace annety_crc

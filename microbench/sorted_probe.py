@@ -2,11 +2,10 @@
 """Stage costs of the length-sorted path on BASELINE config 3, with the A/B build of the library
 (python -m annety_amd.build --ab -> microbench/libannety_crc_ab.so, loaded through ANNETY_CRC_LIB). Each setting
 runs in a child process (the library reads its switches once):
-  ANNETY_CRC_SORTED_CLASSES: bit 0 = the >= 9-line class (var_class_w8), bit 1 = the <= 8-line class
-  ANNETY_CRC_W8_PROBE: 1 = every step unmasked, 2 = no fold (wrong digests)
+  ANNETY_CRC_W8_PROBE: 0 = the product kernel, 1 = every step unmasked, 2 = no fold, 6 = no fold on config 1's
+  window (wrong digests)
 Per setting: microseconds per crc32_batch_var call (HIP events over 200 calls, median of 5 groups), alternating
-settings twice. Usage: python microbench/sorted_probe.py [settings...], a setting = "classes:probe" (default:
-3:0 1:0 2:0 3:1 3:2)."""
+settings twice. Usage: python microbench/sorted_probe.py [probes...] (default: 0 1 2)."""
 import json
 import os
 import subprocess
@@ -54,18 +53,16 @@ def child():
 def main():
     if os.environ.get("SORTED_PROBE_CHILD"):
         return child()
-    settings = sys.argv[1:] or ["3:0", "1:0", "2:0", "3:1", "3:2"]
+    settings = sys.argv[1:] or ["0", "1", "2"]
     lib = os.path.join(ROOT, "microbench", "libannety_crc_ab.so")
     for rep in range(2):
-        for st in settings:
-            cl, pr = st.split(":")
-            env = dict(os.environ, SORTED_PROBE_CHILD="1", ANNETY_CRC_LIB=lib, ANNETY_CRC_SORTED_CLASSES=cl,
-                       ANNETY_CRC_W8_PROBE=pr)
+        for pr in settings:
+            env = dict(os.environ, SORTED_PROBE_CHILD="1", ANNETY_CRC_LIB=lib, ANNETY_CRC_W8_PROBE=pr)
             r = subprocess.run([sys.executable, os.path.abspath(__file__)], env=env, capture_output=True, text=True,
                                timeout=300)
             line = [x for x in r.stdout.splitlines() if x.startswith("{")]
             res = json.loads(line[-1]) if line else {"error": r.stderr[-500:]}
-            print(f"rep {rep} classes {cl} probe {pr}: {res}", flush=True)
+            print(f"rep {rep} probe {pr}: {res}", flush=True)
     return 0
 
 
