@@ -103,6 +103,7 @@ struct StitchGeo {
   size_t n;
   uint64_t zero_line;
   uint32_t* out;
+  uint8_t* ok;            // ArenaLaunch::ok (read only by the VER stitch)
   const uint64_t* check;  // ArenaLaunch::check
   uint32_t check_parts;
   uint64_t check_lo, check_hi;
@@ -129,6 +130,9 @@ struct Vals {
   uint4 h[4], t[4];
   uint32_t x[4], y[4], mid[kMidChunk];
   uint32_t s0;
+  uint32_t tr0, tr1;  // VER: the two dwords holding the trailer
+  uint32_t tsh;       // VER: the trailer's byte offset inside tr0
+  __device__ __forceinline__ uint32_t tr_shift() const { return tsh; }
 };
 
 // The per-payload stitch (file comment). Phase A issues everything the line pass did not write, phase
@@ -137,11 +141,25 @@ struct Vals {
 //   3 = + window folds (no map steps) - wrong digests, used to measure what the stages cost.
 //   MID (A/B): 1 = the whole superblocks between join in one level (mid_level), 0 = a chain of
 //   dependent shift_8KiB steps.
-template <bool UPD, int PROBE, bool MID = false>
+//   VER: LengthHeaderCodec verify (LengthHeaderCodec::decode, include/codec/LengthHeaderCodec.h:107-121): the
+//   4-byte big-endian trailer after each payload is loaded with the plan and compared with the digest here,
+//   ok[p] = 1 on a match (the digest itself is stored only when out is set).
+template <bool UPD, int PROBE, bool MID = false, bool VER = false>
 struct Stitcher {
   const StitchGeo& g;
   const uint32_t* lds;
   LaneCtx k;
+
+  __device__ __forceinline__ void put(size_t p, uint32_t digest, const Vals& v) const {
+    if constexpr (VER) {
+      if (g.out) g.out[p] = digest;
+      // bytes [E, E + 4) of the trailer's two dwords, as a big-endian integer
+      const uint32_t le = __builtin_amdgcn_alignbyte(v.tr1, v.tr0, v.tr_shift());
+      g.ok[p] = __builtin_bswap32(le) == digest ? 1 : 0;
+    } else {
+      g.out[p] = digest;
+    }
+  }
 
   __device__ __forceinline__ uint32_t word(uint32_t idx) const {
     return gload4((uint64_t)(uintptr_t)g.W0 + 4ull * idx);
@@ -217,6 +235,12 @@ struct Stitcher {
 #pragma unroll
     for (int i = 0; i < 4; i++) v.t[i] = gload16(tsrc + 16 * i);
     v.s0 = UPD ? gload4((uint64_t)(uintptr_t)(g.out + p)) : kInit;
+    if constexpr (VER) {  // the trailer [E, E + 4): the dword holding E and, when it is unaligned, the next one
+      const uint64_t ea = y.E & ~3ull;
+      v.tsh = (uint32_t)(y.E & 3);
+      v.tr0 = gload4(ea);
+      v.tr1 = gload4(v.tsh ? ea + 4 : ea);
+    }
 
     // whole lines I0..I1 (empty when I1 < I0)
     const int64_t I0 = (int64_t)L0 + (y.headX ? 0 : 1), I1 = (int64_t)L1 - (y.tailX ? 0 : 1);
@@ -277,7 +301,7 @@ struct Stitcher {
 
   __device__ __forceinline__ void process(size_t p, const Plan& y, Vals& v) const {
     if (y.len == 0) {  // crc of the empty string is 0; update mode leaves the register alone
-      if constexpr (!UPD) g.out[p] = 0u;
+      if constexpr (!UPD) put(p, 0u, v);
       return;
     }
     if constexpr (PROBE == 1) {
@@ -368,7 +392,7 @@ struct Stitcher {
       }
       acc = unshift(acc, 128 - y.te, lds);  // drop the zero bytes after the payload end
     }
-    g.out[p] = UPD ? acc : ~acc;
+    put(p, UPD ? acc : ~acc, v);
   }
 };
 
@@ -393,7 +417,7 @@ __device__ __forceinline__ void publish_extent(ExtentHint* host, uint64_t lo, ui
 // the same count for every block; the first payload's loads are in flight while the LDS image is staged.
 //   PIPE (microbench A/B, product = 0): 1 = the next payload's loads are issued before the
 //   current one is folded; 2 = a lane's first two payloads' descriptors and plan loads issued together.
-template <bool UPD, int BLK = kStitchBlock, int PROBE = 0, int PIPE = 0, bool MID = false>
+template <bool UPD, int BLK = kStitchBlock, int PROBE = 0, int PIPE = 0, bool MID = false, bool VER = false>
 __global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchGeo g0, const uint4* __restrict__ img_slice,
                                                                  const uint4* __restrict__ img_stitch) {
   __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsStitchImageBytes / 16];
@@ -407,7 +431,7 @@ __global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchGeo g0, c
     if (blockIdx.x == 0 && threadIdx.x == 0 && g.record)  // the next calls' record (crc32_kernels.h)
       publish_extent(g.record, lo, hi, sum, bad, g.record_seq);
   }
-  const Stitcher<UPD, PROBE, MID> st{g, reinterpret_cast<const uint32_t*>(lds4), lane_ctx()};
+  const Stitcher<UPD, PROBE, MID, VER> st{g, reinterpret_cast<const uint32_t*>(lds4), lane_ctx()};
   const size_t per = (g.n + gridDim.x - 1) / gridDim.x;
   const size_t p_end = std::min(g.n, (size_t)(blockIdx.x + 1) * per);
   const size_t p_first = (size_t)blockIdx.x * per + threadIdx.x;
@@ -722,6 +746,7 @@ StitchGeo stitch_geo(const ArenaLaunch& a, const ArenaGeom& geo) {
   s.n = a.n;
   s.zero_line = (uint64_t)(uintptr_t)a.zero_line;
   s.out = a.out;
+  s.ok = a.ok;
   s.check = a.check;
   s.check_parts = a.check_parts;
   s.check_lo = a.check_lo;
@@ -738,6 +763,12 @@ hipError_t launch_stitch_p(const ArenaLaunch& a, hipStream_t stream) {
   const size_t blocks = stitch_blocks(a, BLK);
   const uint4* img_slice = static_cast<const uint4*>(a.img_slice);
   const uint4* img_stitch = static_cast<const uint4*>(a.img_stitch);
+  if (a.ok && !a.update) {  // LengthHeaderCodec verify: the trailer compare in the stitch
+    note_kernel("crc32_arena_stitch_kernel<verify>");
+    hipLaunchKernelGGL((crc32_arena_stitch_kernel<false, BLK, PROBE, PIPE, MID, true>), dim3((unsigned)blocks),
+                       dim3(BLK), 0, stream, s, img_slice, img_stitch);
+    return hipGetLastError();
+  }
   note_kernel("crc32_arena_stitch_kernel");
   if (a.update)
     hipLaunchKernelGGL((crc32_arena_stitch_kernel<true, BLK, PROBE, PIPE, MID>), dim3((unsigned)blocks), dim3(BLK), 0,
@@ -784,6 +815,10 @@ hipError_t launch_arena(const ArenaLaunch& a, hipStream_t stream) {
 #ifdef ANNETY_CRC_AB
   static const bool pipe = ANNETY_AB_KNOB("ANNETY_CRC_STITCH_PIPE", 1) != 0;
   static const bool mid = ANNETY_AB_KNOB("ANNETY_CRC_STITCH_MID", 0) == 1;
+  static const int probe = ANNETY_AB_KNOB("ANNETY_CRC_STITCH_PROBE", 0);  // Stitcher PROBE (wrong digests)
+  if (probe == 1) return launch_stitch_p<1, 1>(a, stream);
+  if (probe == 2) return launch_stitch_p<2, 1>(a, stream);
+  if (probe == 3) return launch_stitch_p<3, 1>(a, stream);
   if (mid) return launch_stitch_p<0, 0, kStitchBlock, true>(a, stream);
   if (!pipe) return launch_stitch_p<0>(a, stream);
 #endif

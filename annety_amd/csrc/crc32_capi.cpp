@@ -638,14 +638,17 @@ void arena_fill(const DeviceCtx& c, const void* d_base, size_t arena_bytes, Aren
   arena_fill_range(c, d_base, lo, lo + arena_bytes, a);
 }
 
+// d_ok: LengthHeaderCodec verify - the stitch compares every digest with the trailer after its payload and writes
+// the verdicts (d_out may then be null: no digests)
 int run_arena(DeviceCtx& c, const void* d_base, size_t arena_bytes, const uint64_t* d_off, const uint32_t* d_len,
-              size_t n, uint32_t* d_out, hipStream_t stream, bool update) {
+              size_t n, uint32_t* d_out, hipStream_t stream, bool update, uint8_t* d_ok = nullptr) {
   ArenaLaunch a{};
   arena_fill(c, d_base, arena_bytes, a);
   a.off = d_off;
   a.len = d_len;
   a.n = n;
   a.out = d_out;
+  a.ok = d_ok;
   a.update = update;
   if (n == 0) return ANNETY_CRC_OK;
   if (!a.nsb) {
@@ -1235,10 +1238,11 @@ static int lhc_verify(const void* d_stream, size_t stream_bytes, bool arena, con
   int rc = stream_ctx(static_cast<hipStream_t>(stream), &c);
   if (rc) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
+  // arena: the stitch compares the trailers itself (crc32_arena.hip Stitcher VER), digests only if asked for
+  if (arena) return run_arena(*c, d_stream, stream_bytes, d_payload_off, d_payload_len, n, d_digest, s, false, d_ok);
   uint32_t* dig = d_digest;
   if (!dig) HIP_TRY(hipMallocAsync(reinterpret_cast<void**>(&dig), n * sizeof(uint32_t), s));
-  rc = arena ? run_arena(*c, d_stream, stream_bytes, d_payload_off, d_payload_len, n, dig, s, false)
-             : annety_crc32_batch_var(d_stream, d_payload_off, d_payload_len, n, dig, stream);
+  rc = annety_crc32_batch_var(d_stream, d_payload_off, d_payload_len, n, dig, stream);
   if (rc == ANNETY_CRC_OK) {
     hipError_t e = launch_lhc_compare(d_stream, d_payload_off, d_payload_len, n, dig, d_ok, s);
     if (e != hipSuccess) rc = hip_fail(e);
@@ -1446,15 +1450,9 @@ static int verify_host_iov(const FrameRules& r, const void* const* h_bufs, const
     hipError_t e = hipMemcpyAsync(d_off, st.h_meta, nf * 12, hipMemcpyHostToDevice, s);  // off then len
     if (e != hipSuccess) return fail(hip_fail(e));
     if ((rc = stage_sync(s))) return fail(rc);
-    set_stage("arena verify");
-    rc = run_arena(*c, st.d_stream, total, d_off, d_len, nf, d_dig, s, false);
+    set_stage("arena verify");  // (the stitch compares the trailers: no digests kept)
+    rc = run_arena(*c, st.d_stream, total, d_off, d_len, nf, nullptr, s, false, d_ok);
     if (rc == ANNETY_CRC_OK) rc = stage_sync(s);
-    if (rc == ANNETY_CRC_OK) {
-      set_stage("trailer compare");
-      e = launch_lhc_compare(st.d_stream, d_off, d_len, nf, d_dig, d_ok, s);
-      if (e != hipSuccess) rc = hip_fail(e);
-      if (rc == ANNETY_CRC_OK) rc = stage_sync(s);
-    }
     if (rc == ANNETY_CRC_OK) {
       set_stage("verdict download");
       e = hipMemcpyAsync(st.h_meta + nf * 12, d_ok, nf, hipMemcpyDeviceToHost, s);

@@ -106,7 +106,10 @@ struct ArenaLaunch {
   const void* img_sb;        // superblock join, kLdsSbJoinBytes, then the half-line join byte tables
   const void* img_stitch;    // stitch maps, kLdsStitchImageBytes - kLdsCommonBytes
   const void* zero_line;     // 128 zero bytes (device), read in place of lines outside the arena
-  uint32_t* out;             // digests, or (update) registers in place
+  uint32_t* out;             // digests, or (update) registers in place; may be null when ok is set
+  // LengthHeaderCodec verify (crc32_frames.hip): ok[p] = (digest == the big-endian 4-byte trailer at the payload's
+  // end), written by the stitch; null = digests only
+  uint8_t* ok;
   size_t max_blocks;
   bool update;
   // automatic path selection (annety_crc32_batch_var): the arena was declared from an earlier call's

@@ -4,6 +4,8 @@
 runs in a child process (the library reads its switches once):
   ANNETY_CRC_W8_PROBE: 0 = the product kernel, 1 = every step unmasked, 2 = no fold, 6 = no fold on config 1's
   window (wrong digests)
+  ANNETY_CRC_STITCH_PROBE (the same number, for the arena path, PROBE_PATH=auto on a dense batch): 1 = descriptors
+  and stores only, 2 = + every load, 3 = + the window folds (wrong digests)
 Per setting: microseconds per crc32_batch_var call (HIP events over 200 calls, median of 5 groups), alternating
 settings twice. Usage: python microbench/sorted_probe.py [probes...] (default: 0 1 2)."""
 import json
@@ -24,7 +26,7 @@ def child():
 
     dev = torch.device("cuda", 0)
     lens, offs = bench.zipf_batch(0x5EED)
-    if os.environ.get("PROBE_BATCH") == "small":  # 2M frames of 16 B - 1 KiB, shuffled
+    if os.environ.get("PROBE_BATCH") == "small":  # 2M payloads of 16 B - 1 KiB, packed
         rng = np.random.default_rng(7)
         lens = rng.integers(16, 1025, 2 << 20)
         offs = np.concatenate([[0], np.cumsum(lens)[:-1]])
@@ -33,7 +35,7 @@ def child():
     data = torch.randint(0, 256, (int(lens.sum()),), dtype=torch.uint8, device=dev, generator=g)
     d_off = torch.from_numpy(offs.astype(np.int64)).to(dev)
     d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
-    annety_amd.set_var_path("sorted")
+    annety_amd.set_var_path(os.environ.get("PROBE_PATH", "sorted"))  # auto: the arena for a dense batch
     out = torch.empty(len(lens), dtype=torch.int32, device=dev)
     for _ in range(20):
         annety_amd.crc32_batch_var(data, d_off, d_len, out=out)
@@ -57,7 +59,8 @@ def main():
     lib = os.path.join(ROOT, "microbench", "libannety_crc_ab.so")
     for rep in range(2):
         for pr in settings:
-            env = dict(os.environ, SORTED_PROBE_CHILD="1", ANNETY_CRC_LIB=lib, ANNETY_CRC_W8_PROBE=pr)
+            env = dict(os.environ, SORTED_PROBE_CHILD="1", ANNETY_CRC_LIB=lib, ANNETY_CRC_W8_PROBE=pr,
+                       ANNETY_CRC_STITCH_PROBE=pr)
             r = subprocess.run([sys.executable, os.path.abspath(__file__)], env=env, capture_output=True, text=True,
                                timeout=300)
             line = [x for x in r.stdout.splitlines() if x.startswith("{")]
