@@ -1275,7 +1275,7 @@ static int encode_batch(const FrameRules& r, const void* d_src, const uint64_t* 
   hipStream_t s = static_cast<hipStream_t>(stream);
   // one pass: each payload read once, its frame (header, copy, CRC trailer) written once (crc32_frames.hip)
   HIP_TRY(launch_lhc_encode_fused(d_src, d_src_off, d_len, n, r.T, r.enc_min, r.enc_max, d_dst, d_frame_off, c->d_zero,
-                                  c->d_slice, group_image(*c, 8), c->d_unshift, grid_cus(*c), s));
+                                  c->d_slice, c->d_w8, grid_cus(*c), s));
   return ANNETY_CRC_OK;
 }
 

@@ -232,6 +232,37 @@ __device__ __forceinline__ void gstore4(uint64_t addr, uint32_t v) { *(__attribu
 __device__ __forceinline__ void gstore1(uint64_t addr, uint32_t v) {
   *(__attribute__((address_space(1))) uint8_t*)addr = (uint8_t)v;
 }
+// (any byte address: the hardware runs unaligned global stores, microbench/ua_store_mb.hip - exact, 0.96-0.98 of the
+// aligned rate for 16-byte stores)
+__device__ __forceinline__ void gstore2(uint64_t addr, uint32_t v) {
+  *(__attribute__((address_space(1))) uint16_t*)addr = (uint16_t)v;
+}
+__device__ __forceinline__ void gstore8(uint64_t addr, uint64_t v) { *(__attribute__((address_space(1))) uint64_t*)addr = v; }
+__device__ __forceinline__ void gstore16(uint64_t addr, uint4 v) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 x;
+  x.x = v.x;
+  x.y = v.y;
+  x.z = v.z;
+  x.w = v.w;
+  *(__attribute__((address_space(1))) u32x4*)addr = x;
+}
+
+// lane ^ 8 (DPP row_xmask:8 inside each row of 16)
+__device__ __forceinline__ int32_t lane_xor8(int32_t x) { return __builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, false); }
+// shift_{-m}, m in [0, 128): U_hi[m >> 4] o U_lo[m & 15] from the w8 image (crc32_math.h kLdsW8UnshiftOff)
+__device__ __forceinline__ uint32_t w8_unshift(uint32_t t, uint32_t m, const uint32_t* lds) {
+  t = nibble_map_uniform(t, lds, kLdsW8UnshiftOff + (m & 15u) * 512);
+  return nibble_map_uniform(t, lds, kLdsW8UnshiftOff + 8192 + (m >> 4) * 512);
+}
+// shift_{(7-j)*128} from the w8 image's unreplicated join tables
+__device__ __forceinline__ uint32_t w8_join(uint32_t s, const uint32_t* lds, uint32_t j) {
+  const uint32_t* t = lds + kLdsW8JoinOff / 4 + j;
+  uint32_t r[8];
+#pragma unroll
+  for (int k = 0; k < 8; k++) r[k] = t[k * 128 + __builtin_amdgcn_ubfe(s, 4 * k, 4) * 8];
+  return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6] ^ r[7]);
+}
 
 // The streaming loops raise their wave priority while they issue the next task's loads, so the
 // other wave on the SIMD (in its fold) does not delay them: config-1 kernel -0.5..1.0 %, arena line

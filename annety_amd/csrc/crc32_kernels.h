@@ -215,11 +215,11 @@ hipError_t launch_arena_lines(const ArenaLaunch& a, hipStream_t stream);
 hipError_t launch_lhc_compare(const void* stream_base, const uint64_t* off, const uint32_t* len, size_t n,
                               const uint32_t* digest, uint8_t* ok, hipStream_t stream);
 // One pass per frame: CRC, header, payload copy and trailer (crc32_frames.hip lhc_encode_fused_kernel). zero_line:
-// 128 zero bytes (device); img_g8 = the G = 8 group part of the var image.
+// 128 zero bytes (device); img_w8 = the sorted path's image part (kW8ImgBytes, crc32_math.h).
 hipError_t launch_lhc_encode_fused(const void* src, const uint64_t* src_off, const uint32_t* len, size_t n, int T,
                                    int64_t enc_min, int64_t enc_max, void* dst, const uint64_t* dst_off,
-                                   const void* zero_line, const void* img_slice, const void* img_g8,
-                                   const void* img_unshift, size_t max_blocks, hipStream_t stream);
+                                   const void* zero_line, const void* img_slice, const void* img_w8,
+                                   size_t max_blocks, hipStream_t stream);
 int fixed_kernel_block();
 // Records, for annety_crc_last_kernels, that the current entry point enqueued `name` (crc32_capi.cpp).
 void note_kernel(const char* name);

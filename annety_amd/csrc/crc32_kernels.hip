@@ -605,8 +605,6 @@ __device__ __forceinline__ void var_class(uint4* lds4, const uint8_t* __restrict
   }
 }
 
-__device__ __forceinline__ int32_t lane_xor8(int32_t x) { return __builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, false); }
-
 template <int G, bool SORTED, bool UPD = false, int VWG = kVwg, int PROBE = 0>
 __global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __restrict__ base, size_t n,
                                                            uint64_t fstride, uint32_t flen,
@@ -668,19 +666,7 @@ __device__ __forceinline__ W8Task decode_w8(uint4 d, bool valid) {
   k.valid = valid;
   return k;
 }
-// shift_{-m}, m in [0, 128): U_hi[m >> 4] o U_lo[m & 15] from the w8 image
-__device__ __forceinline__ uint32_t w8_unshift(uint32_t t, uint32_t m, const uint32_t* lds) {
-  t = nibble_map_uniform(t, lds, kLdsW8UnshiftOff + (m & 15u) * 512);
-  return nibble_map_uniform(t, lds, kLdsW8UnshiftOff + 8192 + (m >> 4) * 512);
-}
-// shift_{(7-j)*128} from the unreplicated join tables
-__device__ __forceinline__ uint32_t w8_join(uint32_t s, const uint32_t* lds, uint32_t j) {
-  const uint32_t* t = lds + kLdsW8JoinOff / 4 + j;
-  uint32_t r[8];
-#pragma unroll
-  for (int k = 0; k < 8; k++) r[k] = t[k * 128 + __builtin_amdgcn_ubfe(s, 4 * k, 4) * 8];
-  return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6] ^ r[7]);
-}
+// (w8_unshift, w8_join, lane_xor8: crc32_device.h)
 
 //   PROBE (A/B builds only, microbench/sorted_probe.py; product = 0): bit 0 = every step takes the unmasked
 //   branch, bit 1 = no fold (the data are xored into the register), bit 2 = loads from config 1's window (wave w,

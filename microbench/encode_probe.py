@@ -1,0 +1,78 @@
+#!/usr/bin/env python3
+"""Stage costs of the fused LengthHeaderCodec encode (crc32_frames.hip lhc_encode_fused_kernel) on bench.py's frames
+workload (2M payloads of 16 B - 1 KiB, or 408 B with ENC_FRAMES=chat), with the A/B build of the library
+(python -m annety_amd.build --ab -> microbench/libannety_crc_ab.so, loaded through ANNETY_CRC_LIB):
+  ANNETY_CRC_ENC_PROBE: 0 = the product kernel, 1 = no copy stores, 2 = no CRC, 3 = neither (wrong frames)
+Per setting: microseconds per annety_lhc_encode_batch (HIP events over 200 calls, median of 5 groups), in a child
+process each, alternating twice. Usage: python microbench/encode_probe.py [probes...] (default: 0 1 2 3)."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def child():
+    import numpy as np
+    import torch
+
+    import annety_amd
+    from annety_amd import _lib
+
+    dev = torch.device("cuda", 0)
+    rng = np.random.default_rng(0xF4A3E5)
+    n = 2 << 20
+    lens = np.full(n, 408, dtype=np.int64) if os.environ.get("ENC_FRAMES") == "chat" else rng.integers(16, 1025, n)
+    src_off = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    g = torch.Generator(device=dev)
+    g.manual_seed(4242)
+    src = torch.randint(0, 256, (int(lens.sum()),), dtype=torch.uint8, device=dev, generator=g)
+    frame_off = np.concatenate([[0], np.cumsum(lens + 8)[:-1]]).astype(np.int64)
+    out = torch.empty(int((lens + 8).sum()), dtype=torch.uint8, device=dev)
+    d_src_off = torch.from_numpy(src_off).to(dev)
+    d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
+    d_foff = torch.from_numpy(frame_off).to(dev)
+    lib = _lib.get()
+    s = torch.cuda.current_stream().cuda_stream
+
+    def call():
+        st = lib.annety_lhc_encode_batch(src.data_ptr(), d_src_off.data_ptr(), d_len.data_ptr(), n, 4, 1 << 20,
+                                         out.data_ptr(), d_foff.data_ptr(), s)
+        if st:
+            _lib.check(st, "annety_lhc_encode_batch")
+
+    for _ in range(20):
+        call()
+    torch.cuda.synchronize()
+    per = []
+    for _ in range(5):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(200):
+            call()
+        e1.record()
+        torch.cuda.synchronize()
+        per.append(e0.elapsed_time(e1) / 200 * 1e3)
+    print(json.dumps({"us": sorted(per)[2], "kernels": annety_amd.last_kernels()}))
+
+
+def main():
+    if os.environ.get("ENC_PROBE_CHILD"):
+        return child()
+    settings = sys.argv[1:] or ["0", "1", "2", "3"]
+    lib = os.path.join(ROOT, "microbench", "libannety_crc_ab.so")
+    for rep in range(2):
+        for pr in settings:
+            env = dict(os.environ, ENC_PROBE_CHILD="1", ANNETY_CRC_LIB=lib, ANNETY_CRC_ENC_PROBE=pr)
+            r = subprocess.run([sys.executable, os.path.abspath(__file__)], env=env, capture_output=True, text=True,
+                               timeout=300)
+            line = [x for x in r.stdout.splitlines() if x.startswith("{")]
+            res = json.loads(line[-1]) if line else {"error": r.stderr[-500:]}
+            print(f"rep {rep} probe {pr}: {res}", flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
