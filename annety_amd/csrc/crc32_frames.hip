@@ -76,10 +76,12 @@ __device__ __forceinline__ uint64_t encw_round(const EncW& k, uint32_t r) {
   return k.a0 + (r == 0 ? 0ull : (uint64_t)k.h * 128u + (uint64_t)(r - 1) * 1024u);
 }
 
+// 768 lanes per block: 3 waves per SIMD (<= 168 VGPRs) over the one LDS image.
+constexpr int kEncBlock = 768;
 //   PROBE (A/B builds only, microbench: wrong frames): bit 0 = no copy stores, bit 1 = no CRC (the data are xored
 //   into the register, the trailer still stored).
 template <int PROBE = 0>
-__global__ __launch_bounds__(kBlock) void lhc_encode_fused_kernel(const uint8_t* __restrict__ src,
+__global__ __launch_bounds__(kEncBlock) void lhc_encode_fused_kernel(const uint8_t* __restrict__ src,
                                                                   const uint64_t* __restrict__ src_off,
                                                                   const uint32_t* __restrict__ len, size_t n, int T,
                                                                   int64_t enc_min, int64_t enc_max,
@@ -92,8 +94,8 @@ __global__ __launch_bounds__(kBlock) void lhc_encode_fused_kernel(const uint8_t*
   __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsW8ImageBytes / 16];
   const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
   const uint32_t l = threadIdx.x & 63, l3 = (l >> 3) & 1, j = l & 7;
-  const size_t gid = group_id<kBlock, G, kVwg>();
-  const size_t ngroups = ((size_t)gridDim.x * kBlock) / G;
+  const size_t gid = group_id<kEncBlock, G, kVwg>();
+  const size_t ngroups = ((size_t)gridDim.x * kEncBlock) / G;
   LaneCtx k;
   k.L0 = (threadIdx.x & 31) << 3;
   k.L1 = k.L0 | (1u << 16);
@@ -143,7 +145,7 @@ __global__ __launch_bounds__(kBlock) void lhc_encode_fused_kernel(const uint8_t*
   load(dL, 0, A, pA);
   EncW dC = dL;
   uint32_t rC = 0, rL = 1;
-  load_image<kLdsW8ImageBytes, kBlock, kLdsCommonBytes>(lds4, img_slice, nullptr, img_w8);
+  load_image<kLdsW8ImageBytes, kEncBlock, kLdsCommonBytes>(lds4, img_slice, nullptr, img_w8);
   __syncthreads();
 
   // bytes [lo, hi) of x (lo < hi <= 16) to addr .. addr + hi - lo, as 8/4/2/1-byte pieces
@@ -321,11 +323,11 @@ hipError_t launch_lhc_encode_fused(const void* src, const uint64_t* src_off, con
                                    const void* zero_line, const void* img_slice, const void* img_w8,
                                    size_t max_blocks, hipStream_t stream) {
   if (n == 0) return hipSuccess;
-  const size_t want = (n * 8 + kBlock - 1) / kBlock;
+  const size_t want = (n * 8 + kEncBlock - 1) / kEncBlock;
   const unsigned blocks = (unsigned)std::max<size_t>(1, std::min(max_blocks, want));
   note_kernel("lhc_encode_fused_kernel");
 #define ANNETY_ENC_LAUNCH(P)                                                                                        \
-  hipLaunchKernelGGL(lhc_encode_fused_kernel<P>, dim3(blocks), dim3(kBlock), 0, stream,                             \
+  hipLaunchKernelGGL(lhc_encode_fused_kernel<P>, dim3(blocks), dim3(kEncBlock), 0, stream,                             \
                      static_cast<const uint8_t*>(src), src_off, len, n, T, enc_min, enc_max, static_cast<uint8_t*>(dst), \
                      dst_off, (uint64_t)(uintptr_t)zero_line, static_cast<const uint4*>(img_slice),                 \
                      static_cast<const uint4*>(img_w8))
