@@ -43,9 +43,10 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.
 # Per-launch HBM bytes from the rocprofv3 PMC passes of this bench's own command (profiles/pmc.sh, FETCH_SIZE x2
 # gfx950 correction + WRITE_SIZE), committed per config; reported as `traffic` with the file as its source
 # (a PMC pass cannot run inside the timed process).
-PMC_FILES_VAR = {"sorted": "profiles/r04/config3_sorted_pmc.json"}  # config 3 on another variable path
-PMC_FILES_FRAMES = {}  # --config frames: (variant, op) -> committed PMC summary
-PMC_FILES = {1: "profiles/r04/config1_pmc.json", 3: "profiles/r04/config3_pmc.json",
+PMC_FILES_VAR = {"sorted": "profiles/r05/pmc/c3s.json"}  # config 3 on another variable path
+PMC_FILES_FRAMES = {("mixed", "verify"): "profiles/r05/pmc/fmv.json", ("mixed", "encode"): "profiles/r05/pmc/fme.json",
+                    ("chat", "verify"): "profiles/r05/pmc/fcv.json", ("chat", "encode"): "profiles/r05/pmc/fce.json"}
+PMC_FILES = {1: "profiles/r04/config1_pmc.json", 3: "profiles/r05/pmc/c3a.json",
              2: "profiles/r04/config2_pmc.json", 4: "profiles/r04/config1_pmc.json"}
 CPU_SAMPLE_BYTES = 1 << 30  # cpu_baseline sample: up to 1 GiB of the workload, far above the host's caches
 # The reference build of oracle/_ref (oracle/Makefile): the reference's Release flags without -march=native.
@@ -505,7 +506,11 @@ def pmc_traffic(w: Workload, var_path: str):
             d = json.load(f)
     except (OSError, ValueError):
         return None
-    tot = sum(v.get("hbm_bytes_per_launch", 0) for k, v in d.items() if "crc32_" in k or "lhc_" in k)
+    # the kernels of one step: the library's own list for it (a summary also holds the setup's launches, e.g. the
+    # encode that builds the frames stream of a verify step), by name without template arguments
+    step = {x.split("<")[0].strip() for x in (w.kernel or "").split("+") if x.strip()}
+    tot = sum(v.get("hbm_bytes_per_launch", 0) for k, v in d.items()
+              if ("crc32_" in k or "lhc_" in k) and (not step or k.split("<")[0].strip() in step))
     if not tot:
         return None
     if w.config == 4:  # the config-1 measurement is per 1M payloads; a config-4 step is n/1M of them
