@@ -48,9 +48,12 @@ __global__ __launch_bounds__(256) void lhc_compare_kernel(const uint8_t* __restr
 // gave them none); they read the library's zero line. Algorithmic traffic: the payload read once, the frame
 // written once.
 struct EncW {
-  uint64_t A, E, a0, Dp;  // payload [A, E), its virtual line 0, payload destination (frame start + T)
-  uint32_t L, lead, te, h, R;
+  uint64_t A, Dp;  // payload [A, E = A + L), payload destination (frame start + T)
+  uint32_t L, te, h, R;
   bool live, valid;  // live: an index of the batch; valid: a frame to write
+  __device__ __forceinline__ uint64_t E() const { return A + L; }
+  __device__ __forceinline__ uint64_t a0() const { return A & ~15ull; }  // virtual line 0
+  __device__ __forceinline__ uint32_t lead() const { return (uint32_t)A & 15u; }
 };
 __device__ __forceinline__ EncW decode_encw(const uint8_t* src, uint8_t* dst, uint64_t soff, uint32_t L,
                                             uint64_t foff, int T, int64_t enc_min, int64_t enc_max, bool live,
@@ -60,11 +63,8 @@ __device__ __forceinline__ EncW decode_encw(const uint8_t* src, uint8_t* dst, ui
   k.valid = live && L > 0 && (int64_t)L >= enc_min && !(enc_max > 0 && (int64_t)L > enc_max);
   k.L = k.valid ? L : 16u;  // (16 bytes of the zero line)
   k.A = k.valid ? (uint64_t)(uintptr_t)(src + soff) : zero_line;
-  k.E = k.A + k.L;
-  k.a0 = k.A & ~15ull;
   k.Dp = (uint64_t)(uintptr_t)(dst + foff) + (uint32_t)T;
-  k.lead = (uint32_t)(k.A - k.a0);
-  const uint64_t span = (uint64_t)k.lead + k.L;
+  const uint64_t span = (uint64_t)k.lead() + k.L;
   const uint32_t nl = (uint32_t)((span + 127) >> 7);
   k.te = (uint32_t)(span - 128ull * (nl - 1));
   k.h = ((nl - 1) & 7u) + 1;
@@ -73,11 +73,12 @@ __device__ __forceinline__ EncW decode_encw(const uint8_t* src, uint8_t* dst, ui
 }
 // round r's first byte
 __device__ __forceinline__ uint64_t encw_round(const EncW& k, uint32_t r) {
-  return k.a0 + (r == 0 ? 0ull : (uint64_t)k.h * 128u + (uint64_t)(r - 1) * 1024u);
+  return k.a0() + (r == 0 ? 0ull : (uint64_t)k.h * 128u + (uint64_t)(r - 1) * 1024u);
 }
 
-// 768 lanes per block: 3 waves per SIMD (<= 168 VGPRs) over the one LDS image.
-constexpr int kEncBlock = 768;
+// 512 lanes per block (2 waves per SIMD over the one LDS image). 768 lanes (3 per SIMD) measured 0.588 against
+// 0.637 ms on chat frames and 0.676 against 0.682 on mixed ones, but spill (the kernel needs ~175 VGPRs of 168).
+constexpr int kEncBlock = 512;
 //   PROBE (A/B builds only, microbench: wrong frames): bit 0 = no copy stores, bit 1 = no CRC (the data are xored
 //   into the register, the trailer still stored).
 template <int PROBE = 0>
@@ -117,8 +118,8 @@ __global__ __launch_bounds__(kEncBlock) void lhc_encode_fused_kernel(const uint8
   // (the partial chunks, stored piecewise), the other lanes the round's first chunk (unused)
   auto load = [&](const EncW& tk, uint32_t r, uint4 (&v)[8], uint4& pc) __attribute__((always_inline)) {
     const uint64_t rb = encw_round(tk, r);
-    pc = gload16(j == 0 && r == 0 ? tk.a0 : (j == 1 && r + 1 == tk.R ? (tk.E - 1) & ~15ull : rb));
-    const uint64_t last = ((tk.E - 1) & ~15ull) - rb;
+    pc = gload16(j == 0 && r == 0 ? tk.a0() : (j == 1 && r + 1 == tk.R ? (tk.E() - 1) & ~15ull : rb));
+    const uint64_t last = ((tk.E() - 1) & ~15ull) - rb;
     const uint32_t lim = last < 1008u ? (uint32_t)last : 1008u;
     const uint32_t lo = (uint32_t)rb, hi = (uint32_t)(rb >> 32);
 #pragma unroll
@@ -195,7 +196,7 @@ __global__ __launch_bounds__(kEncBlock) void lhc_encode_fused_kernel(const uint8
     if constexpr ((PROBE & 1) == 0) {
       const uint64_t rb = encw_round(cur, r_c);
       const uint64_t drb = rb + (cur.Dp - cur.A);
-      const int64_t lo64 = (int64_t)(cur.A - rb), hi64 = (int64_t)(cur.E - rb);
+      const int64_t lo64 = (int64_t)(cur.A - rb), hi64 = (int64_t)(cur.E() - rb);
       uint32_t plo = lo64 > 0 ? (uint32_t)lo64 : 0u;
       uint32_t phi = hi64 < 1024 ? (uint32_t)hi64 : 1024u;
       if (r_c == 0 && phi > 128u * cur.h) phi = 128u * cur.h;
@@ -212,12 +213,12 @@ __global__ __launch_bounds__(kEncBlock) void lhc_encode_fused_kernel(const uint8
       }
       // the partial chunks: the first (bytes [lead, ...) when the payload does not start on a chunk) by lane 0,
       // the last (bytes [0, E - chunk) when it does not end on one, and it is not the first) by lane 1
-      const uint64_t tc = (cur.E - 1) & ~15ull;
-      const bool hp = live && j == 0 && r_c == 0 && cur.lead > 0;
-      const bool tp = live && j == 1 && r_c + 1 == cur.R && (cur.E & 15) != 0 && !(tc == cur.a0 && cur.lead > 0);
+      const uint64_t tc = (cur.E() - 1) & ~15ull;
+      const bool hp = live && j == 0 && r_c == 0 && cur.lead() > 0;
+      const bool tp = live && j == 1 && r_c + 1 == cur.R && (cur.E() & 15) != 0 && !(tc == cur.a0() && cur.lead() > 0);
       if (__builtin_amdgcn_ballot_w64(hp || tp) != 0) {
-        const uint32_t lo = hp ? cur.lead : 0u;
-        const uint32_t hi = hp ? min(16u, cur.lead + cur.L) : (uint32_t)(cur.E - tc);
+        const uint32_t lo = hp ? cur.lead() : 0u;
+        const uint32_t hi = hp ? min(16u, cur.lead() + cur.L) : (uint32_t)(cur.E() - tc);
         store_piece(hp ? cur.Dp : tc + (cur.Dp - cur.A), pc, lo, hi, hp || tp);
       }
     }
@@ -238,7 +239,7 @@ __global__ __launch_bounds__(kEncBlock) void lhc_encode_fused_kernel(const uint8
     }
     // masked round (var_class_w8): keep bytes [lo, hi) of half q of line j; lanes ^ 8 exchange bounds
     const bool head = live && r_c == 0, last = live && r_c + 1 == cur.R;
-    const int32_t line_lo = head && j == 0 ? (int32_t)cur.lead : 0;
+    const int32_t line_lo = head && j == 0 ? (int32_t)cur.lead() : 0;
     const int32_t line_hi =
         !live || (head && j >= cur.h) ? 0 : (last && j == (head ? cur.h - 1 : 7u) ? (int32_t)cur.te : 128);
     const int32_t lo_own = min(max(line_lo - 64 * (int32_t)l3, 0), 64), hi_own = min(max(line_hi - 64 * (int32_t)l3, 0), 64);
@@ -264,7 +265,7 @@ __global__ __launch_bounds__(kEncBlock) void lhc_encode_fused_kernel(const uint8
       const int src_l = (int)(head ? (from ? l - up : l) : l);
       const uint32_t moved = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * src_l, (int)s);
       s = head ? (from ? moved : 0u) : s;
-      if (head && j == up) s ^= lds[kLdsW8InitOff / 4 + cur.lead];  // shift_{128-lead}(kInit)
+      if (head && j == up) s ^= lds[kLdsW8InitOff / 4 + cur.lead()];  // shift_{128-lead}(kInit)
     }
     if (__builtin_amdgcn_ballot_w64(last) != 0) {
       const uint32_t t = group_xor_reduce<G>(w8_join(s, lds, j));
