@@ -203,3 +203,34 @@ def test_dense_unsorted_or_gapped_batch_moves_to_arena(gpu, layout):
         _check(out, data, offs, lens)
     s1 = annety_amd.var_path_stats(0)
     assert s1["sorted"] - s0["sorted"] == 2 and s1["arena"] - s0["arena"] == 10, (s0, s1)
+
+
+@pytest.mark.parametrize("density,arena", [(0.655, False), (0.680, True)])
+def test_density_boundary_inside_one_allocation(gpu, density, arena):
+    """The 2/3-density rule (crc32_capi.cpp run_var_auto: payload bytes * 3 >= span * 2) pinned from both sides on
+    one allocation: equal 40,000-byte payloads with equal gaps of >= 4 KiB (so the small-gap rule does not apply),
+    at 0.655 of the span the sorted path stays, at 0.680 the arena takes over after the two recording calls.
+    Every digest is exact either way."""
+    import torch
+
+    import annety_amd
+
+    n, L = 1200, 40000
+    gap = int(round(L / density)) - L
+    lens = np.full(n, L, dtype=np.int64)
+    offs = (np.arange(n, dtype=np.int64) * (L + gap)).astype(np.int64)
+    span = int(offs[-1] + L)
+    assert (n * L * 3 >= span * 2) == arena  # the layout is on the intended side of the rule
+    data = np.random.default_rng(11).integers(0, 256, span + 256, dtype=np.uint8)
+    d, o, ln = _dev(gpu, data, offs, lens)
+    out = torch.empty(n, dtype=torch.int32, device=gpu)
+    s0 = annety_amd.var_path_stats(0)
+    for _ in range(6):
+        out.fill_(7)
+        annety_amd.crc32_batch_var(d, o, ln, out=out)
+        _check(out, data, offs, lens)
+    s1 = annety_amd.var_path_stats(0)
+    if arena:
+        assert s1["sorted"] - s0["sorted"] == 2 and s1["arena"] - s0["arena"] == 4, (s0, s1)
+    else:
+        assert s1["arena"] == s0["arena"] and s1["sorted"] - s0["sorted"] == 6, (s0, s1)
