@@ -676,7 +676,9 @@ __global__ __launch_bounds__(kBucketThreads) void crc32_bucket_place(const uint6
 
 unsigned bucket_grid(size_t n) {
   // about one payload per thread (the launches are latency-bound), up to kExtentMaxParts blocks
-  return (unsigned)std::max<size_t>(1, std::min<size_t>((n + kExtentBlock - 1) / kExtentBlock, kExtentMaxParts));
+  static const size_t per = (size_t)std::max(1, ANNETY_AB_KNOB("ANNETY_CRC_BUCKET_PER", 1));  // A/B: payloads per thread
+  const size_t chunk = per * kExtentBlock;
+  return (unsigned)std::max<size_t>(1, std::min<size_t>((n + chunk - 1) / chunk, kExtentMaxParts));
 }
 
 hipError_t launch_extent(const uint64_t* off, const uint32_t* len, size_t n, void* ws, uint32_t* parts,

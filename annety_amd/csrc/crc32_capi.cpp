@@ -230,6 +230,12 @@ const HostImages& host_images() {
       std::memcpy(m + (kLdsW8UnshiftOff - kLdsCommonBytes) / 4, img.unshift.data(), img.unshift.size() * 4);
       for (uint32_t lead = 0; lead < 128; lead++)
         m[(kLdsW8InitOff - kLdsCommonBytes) / 4 + lead] = gf2_apply(shift_matrix(128 - lead), kInit);
+      uint32_t* mk = m + (kLdsW8MaskOff - kLdsCommonBytes) / 4;  // KEEP_FROM[a], then KEEP_TO[b]
+      for (uint32_t a = 0; a <= 16; a++)
+        for (uint32_t byte = 0; byte < 16; byte++) {
+          if (byte >= a) mk[a * 4 + byte / 4] |= 0xFFu << (8 * (byte % 4));
+          if (byte < a) mk[(17 + a) * 4 + byte / 4] |= 0xFFu << (8 * (byte % 4));
+        }
     }
   });
   return img;

@@ -248,6 +248,21 @@ __device__ __forceinline__ void gstore16(uint64_t addr, uint4 v) {
   *(__attribute__((address_space(1))) u32x4*)addr = x;
 }
 
+// Keep bytes [lo, hi) of N 16-byte chunks (N = 4: a half line), zero the rest, from the w8 image's chunk masks
+// (crc32_math.h kLdsW8MaskOff): per chunk two ds_read_b128 and four ands, against mask_line's per-word shifts.
+template <int N>
+__device__ __forceinline__ void mask_chunks(uint4 (&v)[N], int32_t lo, int32_t hi, const uint32_t* lds) {
+  const uint4* t = reinterpret_cast<const uint4*>(lds + kLdsW8MaskOff / 4);
+#pragma unroll
+  for (int i = 0; i < N; i++) {
+    const uint4 a = t[min(max(lo - 16 * i, 0), 16)], b = t[17 + min(max(hi - 16 * i, 0), 16)];
+    v[i].x &= a.x & b.x;
+    v[i].y &= a.y & b.y;
+    v[i].z &= a.z & b.z;
+    v[i].w &= a.w & b.w;
+  }
+}
+
 // lane ^ 8 (DPP row_xmask:8 inside each row of 16)
 __device__ __forceinline__ int32_t lane_xor8(int32_t x) { return __builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, false); }
 // shift_{-m}, m in [0, 128): U_hi[m >> 4] o U_lo[m & 15] from the w8 image (crc32_math.h kLdsW8UnshiftOff)

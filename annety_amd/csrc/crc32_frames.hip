@@ -250,8 +250,8 @@ __global__ __launch_bounds__(kEncBlock) void lhc_encode_fused_kernel(const uint8
     const int32_t lo_b = l3 ? lo_own : lo_par, hi_b = l3 ? hi_own : hi_par;
     if (__builtin_amdgcn_ballot_w64(lo_a > 0 || hi_a < 64 || lo_b > 0 || hi_b < 64) != 0) {
       uint4 va[4] = {v[0], v[1], v[2], v[3]}, vb[4] = {v[4], v[5], v[6], v[7]};
-      mask_line<4>(va, lo_a * 8, hi_a * 8);
-      mask_line<4>(vb, lo_b * 8, hi_b * 8);
+      mask_chunks<4>(va, lo_a, hi_a, lds);
+      mask_chunks<4>(vb, lo_b, hi_b, lds);
 #pragma unroll
       for (int i = 0; i < 4; i++) {
         v[i] = va[i];

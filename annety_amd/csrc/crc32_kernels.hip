@@ -671,8 +671,8 @@ __device__ __forceinline__ W8Task decode_w8(uint4 d, bool valid) {
 //   PROBE (A/B builds only, microbench/sorted_probe.py; product = 0): bit 0 = every step takes the unmasked
 //   branch, bit 1 = no fold (the data are xored into the register), bit 2 = loads from config 1's window (wave w,
 //   step s: 8 KiB at (s W + w) 8 KiB) instead of the tasks' rounds, bit 3 = the same window loaded with config 1's
-//   scalar base and immediate offsets - wrong digests, used to measure what the masked rounds, the fold, the
-//   access pattern and the per-group addressing cost.
+//   scalar base and immediate offsets, bit 4 = masked rounds without their byte masks - wrong digests, used to
+//   measure what the masked rounds, the fold, the access pattern and the per-group addressing cost.
 template <bool UPD, int PROBE = 0>
 __device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restrict__ base,
                                              const uint4* __restrict__ desc, const uint32_t* __restrict__ range,
@@ -835,10 +835,10 @@ __device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restr
     // v[0..3]: the even group of the pair (own if l3 = 0), v[4..7]: the odd one
     const int32_t lo_a = l3 ? lo_par : lo_own, hi_a = l3 ? hi_par : hi_own;
     const int32_t lo_b = l3 ? lo_own : lo_par, hi_b = l3 ? hi_own : hi_par;
-    if (__builtin_amdgcn_ballot_w64(lo_a > 0 || hi_a < 64 || lo_b > 0 || hi_b < 64) != 0) {
+    if ((PROBE & 16) == 0 && __builtin_amdgcn_ballot_w64(lo_a > 0 || hi_a < 64 || lo_b > 0 || hi_b < 64) != 0) {
       uint4 va[4] = {v[0], v[1], v[2], v[3]}, vb[4] = {v[4], v[5], v[6], v[7]};
-      mask_line<4>(va, lo_a * 8, hi_a * 8);
-      mask_line<4>(vb, lo_b * 8, hi_b * 8);
+      mask_chunks<4>(va, lo_a, hi_a, lds);
+      mask_chunks<4>(vb, lo_b, hi_b, lds);
 #pragma unroll
       for (int i = 0; i < 4; i++) {
         v[i] = va[i];
@@ -1114,6 +1114,7 @@ hipError_t launch_var_sorted(const VarLaunch& a, const void* img_w8, hipStream_t
 #ifdef ANNETY_CRC_AB
   static const int probe = ANNETY_AB_KNOB("ANNETY_CRC_W8_PROBE", 0);
   if (!a.update && probe == 1) ANNETY_SORTED_LAUNCH(false, 1);
+  else if (!a.update && probe == 16) ANNETY_SORTED_LAUNCH(false, 16);
   else if (!a.update && probe == 2) ANNETY_SORTED_LAUNCH(false, 2);
   else if (!a.update && probe == 6) ANNETY_SORTED_LAUNCH(false, 6);
   else if (a.update) ANNETY_SORTED_LAUNCH(true, 0);

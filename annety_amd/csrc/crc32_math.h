@@ -149,13 +149,16 @@ constexpr uint32_t kLdsStitchImageBytes = kLdsMidOff + kMidMaps * 512;  // 16384
 //   [kLdsW8RoundOff, +4 KiB)    byte tables of the round advance shift_{7*128}
 //   [kLdsW8UnshiftOff, +12 KiB) U_lo[m] = shift_{-m} (m = 0..15), U_hi[h] = shift_{-16h} (h = 0..7), 512 B each
 //   [kLdsW8InitOff, +512 B)     shift_{128-lead}(kInit), lead = 0..127: the init as a register at line 0's end
+//   [kLdsW8MaskOff, +544 B)     byte masks of a 16-byte chunk: KEEP_FROM[a] = bytes [a, 16), a = 0..16, then
+//                               KEEP_TO[b] = bytes [0, b), b = 0..16 (crc32_device.h mask_chunks)
 constexpr uint32_t kLdsW8JoinOff = kLdsCommonBytes;
 constexpr uint32_t kLdsW8HalfOff = kLdsW8JoinOff + 4096;
 constexpr uint32_t kLdsW8RoundOff = kLdsW8HalfOff + 4096;
 constexpr uint32_t kLdsW8UnshiftOff = kLdsW8RoundOff + 4096;
 constexpr uint32_t kLdsW8InitOff = kLdsW8UnshiftOff + kLdsUnshiftBytes;
-constexpr uint32_t kLdsW8ImageBytes = kLdsW8InitOff + 512;            // 156672
-constexpr uint32_t kW8ImgBytes = kLdsW8ImageBytes - kLdsCommonBytes;  // 25088
+constexpr uint32_t kLdsW8MaskOff = kLdsW8InitOff + 512;
+constexpr uint32_t kLdsW8ImageBytes = kLdsW8MaskOff + 544;            // 157216
+constexpr uint32_t kW8ImgBytes = kLdsW8ImageBytes - kLdsCommonBytes;  // 25632
 // after the image: each wave's ring of 4 claimed sets' descriptors (8 x 16 B a set), their set indices, and the
 // block's set counters (front, back: 2 x 32 bits of one 64-bit word)
 // The sorted kernel's block: 768 threads (12 waves: 3 per SIMD at <= 168 VGPRs) share the one LDS image.
@@ -164,6 +167,6 @@ constexpr uint32_t kW8MaxWaves = 12;
 constexpr uint32_t kLdsW8RingOff = kLdsW8ImageBytes;
 constexpr uint32_t kLdsW8RingSetOff = kLdsW8RingOff + kW8MaxWaves * 4 * 128;
 constexpr uint32_t kLdsW8CounterOff = kLdsW8RingSetOff + kW8MaxWaves * 4 * 4;
-constexpr uint32_t kLdsW8TotalBytes = kLdsW8CounterOff + 16;  // 163024 <= 163840
+constexpr uint32_t kLdsW8TotalBytes = kLdsW8CounterOff + 16;  // 163568 <= 163840
 
 }  // namespace annety_crc
