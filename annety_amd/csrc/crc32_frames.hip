@@ -80,7 +80,7 @@ __device__ __forceinline__ uint64_t encw_round(const EncW& k, uint32_t r) {
 // 0.637 ms on chat frames and 0.676 against 0.682 on mixed ones, but spill (the kernel needs ~175 VGPRs of 168).
 constexpr int kEncBlock = 512;
 //   PROBE (A/B builds only, microbench: wrong frames): bit 0 = no copy stores, bit 1 = no CRC (the data are xored
-//   into the register, the trailer still stored).
+//   into the register, the trailer still stored), bit 2 = no partial-chunk pieces, bit 3 = no whole-chunk stores.
 template <int PROBE = 0>
 __global__ __launch_bounds__(kEncBlock) void lhc_encode_fused_kernel(const uint8_t* __restrict__ src,
                                                                   const uint64_t* __restrict__ src_off,
@@ -209,14 +209,14 @@ __global__ __launch_bounds__(kEncBlock) void lhc_encode_fused_kernel(const uint8
                            (uint32_t)__builtin_amdgcn_readlane((int)dlo, sl);
         const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)plo, sl);
         const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)phi, sl);
-        if (voff >= a && voff + 16 <= b) gstore16(d + voff, v[i]);
+        if ((PROBE & 8) == 0 && voff >= a && voff + 16 <= b) gstore16(d + voff, v[i]);
       }
       // the partial chunks: the first (bytes [lead, ...) when the payload does not start on a chunk) by lane 0,
       // the last (bytes [0, E - chunk) when it does not end on one, and it is not the first) by lane 1
       const uint64_t tc = (cur.E() - 1) & ~15ull;
       const bool hp = live && j == 0 && r_c == 0 && cur.lead() > 0;
       const bool tp = live && j == 1 && r_c + 1 == cur.R && (cur.E() & 15) != 0 && !(tc == cur.a0() && cur.lead() > 0);
-      if (__builtin_amdgcn_ballot_w64(hp || tp) != 0) {
+      if ((PROBE & 4) == 0 && __builtin_amdgcn_ballot_w64(hp || tp) != 0) {
         const uint32_t lo = hp ? cur.lead() : 0u;
         const uint32_t hi = hp ? min(16u, cur.lead() + cur.L) : (uint32_t)(cur.E() - tc);
         store_piece(hp ? cur.Dp : tc + (cur.Dp - cur.A), pc, lo, hi, hp || tp);
@@ -337,6 +337,8 @@ hipError_t launch_lhc_encode_fused(const void* src, const uint64_t* src_off, con
   if (probe == 1) ANNETY_ENC_LAUNCH(1);
   else if (probe == 2) ANNETY_ENC_LAUNCH(2);
   else if (probe == 3) ANNETY_ENC_LAUNCH(3);
+  else if (probe == 6) ANNETY_ENC_LAUNCH(6);
+  else if (probe == 10) ANNETY_ENC_LAUNCH(10);
   else ANNETY_ENC_LAUNCH(0);
 #else
   ANNETY_ENC_LAUNCH(0);
