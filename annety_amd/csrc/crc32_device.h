@@ -263,6 +263,16 @@ __device__ __forceinline__ void mask_chunks(uint4 (&v)[N], int32_t lo, int32_t h
   }
 }
 
+// Nontemporal 16-byte load from scalar base g (an absolute global address, wave-uniform) + lane offset off: the
+// base goes straight to the instruction's SGPR pair (a base rebuilt from a kernel pointer as ptr + (g - ptr) cost
+// six scalar adds per load).
+__device__ __forceinline__ uint4 gload16_nt(uint64_t g, uint32_t off) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  const __attribute__((address_space(1))) u32x4* p = (const __attribute__((address_space(1))) u32x4*)(g + off);
+  const u32x4 x = __builtin_nontemporal_load(p);
+  return make_uint4(x.x, x.y, x.z, x.w);
+}
+
 // lane ^ 8 (DPP row_xmask:8 inside each row of 16)
 __device__ __forceinline__ int32_t lane_xor8(int32_t x) { return __builtin_amdgcn_mov_dpp(x, 0x128, 0xF, 0xF, false); }
 // shift_{-m}, m in [0, 128): U_hi[m >> 4] o U_lo[m & 15] from the w8 image (crc32_math.h kLdsW8UnshiftOff)

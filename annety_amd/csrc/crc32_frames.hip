@@ -102,7 +102,6 @@ __global__ __launch_bounds__(kEncBlock) void lhc_encode_fused_kernel(const uint8
   k.L1 = k.L0 | (1u << 16);
   k.slot4 = 0;
   const uint32_t voff = coalesced_lane_offset(l);  // line j, chunk 4 l3 + 2 l5 + l4 of a group's 1 KiB round
-  const uint64_t b0 = (uint64_t)(uintptr_t)src;
   auto fetch = [&](size_t t, uint64_t& so, uint32_t& ln, uint64_t& fo) __attribute__((always_inline)) {
     const size_t tc = t < n ? t : n - 1;  // unconditional: past the end re-read the last frame's fields
     so = src_off[tc];
@@ -128,8 +127,7 @@ __global__ __launch_bounds__(kEncBlock) void lhc_encode_fused_kernel(const uint8
       const uint64_t g = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, sl) << 32) |
                          (uint32_t)__builtin_amdgcn_readlane((int)lo, sl);
       const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)lim, sl);
-      const v4u32 x = __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(src + (g - b0) + min(voff, c)));
-      v[i] = make_uint4(x.x, x.y, x.z, x.w);
+      v[i] = gload16_nt(g, min(voff, c));
     }
   };
 

@@ -721,10 +721,7 @@ __device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restr
       const uint64_t g = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, src) << 32) |
                          (uint32_t)__builtin_amdgcn_readlane((int)lo, src);
       const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cl, src);
-      const uint8_t* gb = base + (g - b0);
-      const v4u32 x =
-          __builtin_nontemporal_load(reinterpret_cast<const v4u32*>(gb + ((min(j, c) << 7) | (voff & 127u))));
-      v[i] = make_uint4(x.x, x.y, x.z, x.w);
+      v[i] = gload16_nt(g, (min(j, c) << 7) | (voff & 127u));
     }
   };
 

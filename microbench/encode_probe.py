@@ -4,7 +4,8 @@ workload (2M payloads of 16 B - 1 KiB, or 408 B with ENC_FRAMES=chat), with the 
 (python -m annety_amd.build --ab -> microbench/libannety_crc_ab.so, loaded through ANNETY_CRC_LIB):
   ANNETY_CRC_ENC_PROBE: 0 = the product kernel, 1 = no copy stores, 2 = no CRC, 3 = neither (wrong frames)
 Per setting: microseconds per annety_lhc_encode_batch (HIP events over 200 calls, median of 5 groups), in a child
-process each, alternating twice. Usage: python microbench/encode_probe.py [probes...] (default: 0 1 2 3)."""
+process each, alternating twice. ENC_ALIGNED=1 puts each payload at its frame's payload offset in the source, so
+that every store is 16-byte aligned. Usage: python microbench/encode_probe.py [probes...] (default: 0 1 2 3)."""
 import json
 import os
 import subprocess
@@ -26,10 +27,14 @@ def child():
     n = 2 << 20
     lens = np.full(n, 408, dtype=np.int64) if os.environ.get("ENC_FRAMES") == "chat" else rng.integers(16, 1025, n)
     src_off = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
+    frame_off = np.concatenate([[0], np.cumsum(lens + 8)[:-1]]).astype(np.int64)
+    src_bytes = int(lens.sum())
+    if os.environ.get("ENC_ALIGNED"):  # each payload at its frame's payload offset: every 16-byte store aligned
+        src_off = frame_off + 4
+        src_bytes = int((lens + 8).sum())
     g = torch.Generator(device=dev)
     g.manual_seed(4242)
-    src = torch.randint(0, 256, (int(lens.sum()),), dtype=torch.uint8, device=dev, generator=g)
-    frame_off = np.concatenate([[0], np.cumsum(lens + 8)[:-1]]).astype(np.int64)
+    src = torch.randint(0, 256, (src_bytes,), dtype=torch.uint8, device=dev, generator=g)
     out = torch.empty(int((lens + 8).sum()), dtype=torch.uint8, device=dev)
     d_src_off = torch.from_numpy(src_off).to(dev)
     d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
