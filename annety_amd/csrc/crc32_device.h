@@ -247,6 +247,18 @@ __device__ __forceinline__ void gstore16(uint64_t addr, uint4 v) {
   x.w = v.w;
   *(__attribute__((address_space(1))) u32x4*)addr = x;
 }
+// Nontemporal 16-byte store, as an asm statement: beside a temporal store of the same value and address in the
+// other arm of a branch, the compiler merged the two and dropped the nontemporal flag. (The waitcnt pass does not
+// count an asm store; that only makes its later vmcnt waits stricter, and nothing reads these bytes back.)
+__device__ __forceinline__ void gstore16_nt(uint64_t addr, uint4 v) {
+  typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 x;
+  x.x = v.x;
+  x.y = v.y;
+  x.z = v.z;
+  x.w = v.w;
+  asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(addr), "v"(x) : "memory");
+}
 
 // Keep bytes [lo, hi) of N 16-byte chunks (N = 4: a half line), zero the rest, from the w8 image's chunk masks
 // (crc32_math.h kLdsW8MaskOff): per chunk two ds_read_b128 and four ands, against mask_line's per-word shifts.

@@ -80,7 +80,8 @@ __device__ __forceinline__ uint64_t encw_round(const EncW& k, uint32_t r) {
 // 0.637 ms on chat frames and 0.676 against 0.682 on mixed ones, but spill (the kernel needs ~175 VGPRs of 168).
 constexpr int kEncBlock = 512;
 //   PROBE (A/B builds only, microbench: wrong frames): bit 0 = no copy stores, bit 1 = no CRC (the data are xored
-//   into the register, the trailer still stored), bit 2 = no partial-chunk pieces, bit 3 = no whole-chunk stores.
+//   into the register, the trailer still stored), bit 2 = no partial-chunk pieces, bit 3 = no whole-chunk stores,
+//   bit 5 = whole chunks always stored temporally (the product stores those of frames >= 2 KiB nontemporally).
 template <int PROBE = 0>
 __global__ __launch_bounds__(kEncBlock) void lhc_encode_fused_kernel(const uint8_t* __restrict__ src,
                                                                   const uint64_t* __restrict__ src_off,
@@ -207,7 +208,15 @@ __global__ __launch_bounds__(kEncBlock) void lhc_encode_fused_kernel(const uint8
                            (uint32_t)__builtin_amdgcn_readlane((int)dlo, sl);
         const uint32_t a = (uint32_t)__builtin_amdgcn_readlane((int)plo, sl);
         const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)phi, sl);
-        if ((PROBE & 8) == 0 && voff >= a && voff + 16 <= b) gstore16(d + voff, v[i]);
+        // nontemporal for frames of >= 2 KiB (256K frames of 4000 B: 466 against 520 us per call), temporal for
+        // smaller ones, whose edge lines two groups complete in L2 (2M mixed frames: 631 against 666)
+        const bool nt = (uint32_t)__builtin_amdgcn_readlane((int)cur.L, sl) >= 2048u;
+        if ((PROBE & 8) == 0 && voff >= a && voff + 16 <= b) {
+          if ((PROBE & 32) == 0 && nt)
+            gstore16_nt(d + voff, v[i]);
+          else
+            gstore16(d + voff, v[i]);
+        }
       }
       // the partial chunks: the first (bytes [lead, ...) when the payload does not start on a chunk) by lane 0,
       // the last (bytes [0, E - chunk) when it does not end on one, and it is not the first) by lane 1
@@ -336,6 +345,7 @@ hipError_t launch_lhc_encode_fused(const void* src, const uint64_t* src_off, con
   else if (probe == 2) ANNETY_ENC_LAUNCH(2);
   else if (probe == 3) ANNETY_ENC_LAUNCH(3);
   else if (probe == 6) ANNETY_ENC_LAUNCH(6);
+  else if (probe == 32) ANNETY_ENC_LAUNCH(32);
   else if (probe == 10) ANNETY_ENC_LAUNCH(10);
   else ANNETY_ENC_LAUNCH(0);
 #else

@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """Stage costs of the fused LengthHeaderCodec encode (crc32_frames.hip lhc_encode_fused_kernel) on bench.py's frames
-workload (2M payloads of 16 B - 1 KiB, or 408 B with ENC_FRAMES=chat), with the A/B build of the library
+workload (2M payloads of 16 B - 1 KiB, or 408 B with ENC_FRAMES=chat, or 256K of 4000 B with ENC_FRAMES=big), with the A/B build of the library
 (python -m annety_amd.build --ab -> microbench/libannety_crc_ab.so, loaded through ANNETY_CRC_LIB):
   ANNETY_CRC_ENC_PROBE: 0 = the product kernel, 1 = no copy stores, 2 = no CRC, 3 = neither (wrong frames)
 Per setting: microseconds per annety_lhc_encode_batch (HIP events over 200 calls, median of 5 groups), in a child
@@ -25,7 +25,12 @@ def child():
     dev = torch.device("cuda", 0)
     rng = np.random.default_rng(0xF4A3E5)
     n = 2 << 20
-    lens = np.full(n, 408, dtype=np.int64) if os.environ.get("ENC_FRAMES") == "chat" else rng.integers(16, 1025, n)
+    kind = os.environ.get("ENC_FRAMES", "mixed")
+    if kind == "big":  # 256K frames of 4000 B (about the same bytes)
+        n = 256 << 10
+        lens = np.full(n, 4000, dtype=np.int64)
+    else:
+        lens = np.full(n, 408, dtype=np.int64) if kind == "chat" else rng.integers(16, 1025, n)
     src_off = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
     frame_off = np.concatenate([[0], np.cumsum(lens + 8)[:-1]]).astype(np.int64)
     src_bytes = int(lens.sum())
