@@ -624,11 +624,10 @@ __global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __rest
 // with the steady-state round of crc32_onekib_nt_kernel and no per-lane masks or address arithmetic in it.
 //
 // A payload of nl lines (absolute 128-byte lines L0..L1) is cut into R = (nl - h) / 8 + 1 rounds:
-//   round 0 ("head"): lines [0, 8) read start-aligned, of which the first h = ((nl - 1) mod 8) + 1 are the
-//            payload's (bytes before the payload start masked, lines >= h zeroed; a payload of <= 8 lines, R = 1,
-//            re-reads its last line in their place and ends in this round), then each lane's register is
-//            moved (8 - h) lanes up inside its group (ds_bpermute), so that the group holds the head end-aligned,
-//            and the init (or the caller's register) enters as the register shift_{128-lead}(init) of line 0;
+//   round 0 ("head"): the first h = ((nl - 1) mod 8) + 1 lines, end-aligned: lane j reads line j - (8 - h), the
+//            lanes before line 0 re-read line 0 and are zeroed, the bytes before the payload start are masked,
+//            and the init (or the caller's register) enters as the register shift_{128-lead}(init) of line 0
+//            (a payload of <= 8 lines, R = 1, ends in this round);
 //   rounds 1 .. R-1 ("body"): the 1 KiB pieces [h + 8 (r - 1), h + 8 r): whole lines, except that the last
 //            round's line 7 is the payload's last line (bytes after the payload end masked, removed after the
 //            join by the inverse shift of the line's overhang).
@@ -712,16 +711,16 @@ __device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restr
       return;
     }
     const uint32_t lo = (uint32_t)ad, hi = (uint32_t)(ad >> 32);
-    // a payload of <= 8 lines is one round (R = 1) whose lines [h, 8) lie past its end: those lanes re-read its
-    // last line (masked to zero in compute), so no load leaves the payload's lines
-    const uint32_t cl = r == 0 && tk.R == 1 ? tk.h - 1 : 7u;
+    // the head round is end-aligned: lane j holds line j - (8 - h), and the lanes before line 0 re-read line 0
+    // (zeroed in compute), so no load leaves the payload's lines and no line is read twice
+    const uint32_t up = r == 0 ? 8 - tk.h : 0u;
 #pragma unroll
     for (int i = 0; i < 8; i++) {
       const int src = 8 * ((i >> 2) + 2 * (i & 1) + 4 * ((i >> 1) & 1));
       const uint64_t g = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, src) << 32) |
                          (uint32_t)__builtin_amdgcn_readlane((int)lo, src);
-      const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)cl, src);
-      v[i] = gload16_nt(g, (min(j, c) << 7) | (voff & 127u));
+      const uint32_t c = (uint32_t)__builtin_amdgcn_readlane((int)up, src);
+      v[i] = gload16_nt(g, ((j > c ? j - c : 0u) << 7) | (voff & 127u));
     }
   };
 
@@ -820,10 +819,10 @@ __device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restr
     // Masked round. This lane's group (l >> 3): keep bytes [lo, hi) of half q of its line j, for q = l3 (own use)
     // and 1 - l3 (sent to lane ^ 8, whose v holds this group's half 1 - l3 ... = the partner's own half).
     const bool head = cur.valid && r_c == 0, last = cur.valid && r_c + 1 == cur.R;
-    const int32_t line_lo = head && j == 0 ? (int32_t)cur.lead : 0;
-    // (the last line: line 7 of a last round, line h - 1 of a one-round payload's head round)
-    const int32_t line_hi =
-        !cur.valid || (head && j >= cur.h) ? 0 : (last && j == (head ? cur.h - 1 : 7u) ? (int32_t)cur.te : 128);
+    // (end-aligned head round: line 0 in lane 8 - h, the lanes before it zeroed; the last line is always lane 7)
+    const uint32_t up = 8 - cur.h;
+    const int32_t line_lo = head && j == up ? (int32_t)cur.lead : 0;
+    const int32_t line_hi = !cur.valid || (head && j < up) ? 0 : (last && j == 7 ? (int32_t)cur.te : 128);
     const int32_t lo_own = min(max(line_lo - 64 * (int32_t)l3, 0), 64), hi_own = min(max(line_hi - 64 * (int32_t)l3, 0), 64);
     const int32_t lo_oth = min(max(line_lo - 64 * (int32_t)(l3 ^ 1), 0), 64),
                   hi_oth = min(max(line_hi - 64 * (int32_t)(l3 ^ 1), 0), 64);
@@ -843,14 +842,8 @@ __device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restr
       }
     }
     fold(v);
-    // head round: move the registers (8 - h) lanes up inside the group (lines [0, h) become the round's last h
-    // lines), then line 0's register gains the init as a register at the payload start, shift_{128-lead}(init)
+    // head round: line 0's register gains the init as a register at the payload start, shift_{128-lead}(init)
     if (__builtin_amdgcn_ballot_w64(head) != 0) {
-      const uint32_t up = 8 - cur.h;
-      const bool from = head && j >= up;
-      const int src = (int)(head ? (from ? l - up : l) : l);
-      const uint32_t moved = (uint32_t)__builtin_amdgcn_ds_bpermute(4 * src, (int)s);
-      s = head ? (from ? moved : 0u) : s;
       if (head && j == up) {
         if constexpr (UPD) {
           uint32_t x = w8_unshift(cur.state, cur.lead, lds);                       // shift_{-lead}
