@@ -63,9 +63,29 @@ struct VarLaunch {
 };
 
 hipError_t launch_var(const VarLaunch& a, hipStream_t stream);
+// Long payloads on the sorted path (digest mode): a payload of more than kSplitMin bytes runs as end-aligned
+// segments of kSplitSeg bytes (the first takes the remainder), each a task of the sorted list, so that one long
+// payload no longer serialises kSplitSeg/1 KiB rounds per segment on one lane group. A segment's descriptor index
+// is kSegFlag | (kSegFirst if it is the payload's first) | its slot in seg_crc, which receives its raw register
+// (the first from the init, the others from 0); the launch's last block joins them,
+//   crc = ~xor_k shift_{(S-1-k) kSplitSeg}(seg_crc[slot + k])   (powers: crc32_capi.cpp split_powers).
+// Slots and records are claimed in the count step up to kSplitSegCap / kSplitRecCap per call; a payload that
+// finds none runs whole.
+constexpr uint32_t kSplitSeg = 65536;
+constexpr uint32_t kSplitMin = 2 * kSplitSeg;
+constexpr uint32_t kSplitMaxSegs = 16384;      // the power table's reach (crc32_capi.cpp kMaxSegs)
+constexpr uint32_t kSplitSegCap = 1u << 18;    // segment slots per call
+constexpr uint32_t kSplitRecCap = 1u << 15;    // split payloads per call
+constexpr uint32_t kSegFlag = 0x80000000u, kSegFirst = 0x40000000u, kSegIndexMask = 0x3FFFFFFFu;
+struct SortedSplit {
+  uint32_t* seg_crc;           // kSplitSegCap words
+  const uint4* rec;            // kSplitRecCap records {payload, first slot, segments, 0}
+  unsigned long long* ctr;     // this call's counters: [0] slots, [1] records, [2] finished blocks
+  const uint32_t* powers;      // powers[(m-1)*32 + bit] = shift_{m*kSplitSeg}(1 << bit)
+};
 // The sorted path in one launch (a.range[0..1] = the sorted list's bounds in a.desc); img_w8 = the w8 image
 // (kW8ImgBytes, crc32_math.h); a.group, a.img_group and a.img_unshift are ignored.
-hipError_t launch_var_sorted(const VarLaunch& a, const void* img_w8, hipStream_t stream);
+hipError_t launch_var_sorted(const VarLaunch& a, const void* img_w8, const SortedSplit& split, hipStream_t stream);
 
 // Long payloads cut into end-aligned segments (crc32_kernels.hip): descriptors for the variable kernel,
 // then the combine fold with powers[(m-1)*32 + bit] = shift_{m*seg}(1 << bit), m = 1..S-1.
@@ -81,7 +101,7 @@ hipError_t launch_split_join(const uint32_t* seg_crc, size_t n, uint32_t S, cons
 // Written to the device scratch `ws` (kExtentScratchBytes) and to the pinned host record `host`
 // (ExtentHint), whose `chk` = lo ^ hi ^ sum ^ bad ^ seq ^ kExtentCheck lets the host reject a record it read
 // while the device was rewriting it.
-constexpr size_t kExtentScratchBytes = 16384;
+constexpr size_t kExtentScratchBytes = 16384 + 64;  // + the sorted path's two split counter sets (kSplitCtrOff)
 constexpr uint32_t kExtentMaxParts = 128;  // partials (uint64 {lo, hi, sum, bad} at word 8 + 4b)
 constexpr uint64_t kExtentCheck = 0x9E3779B97F4A7C15ull;
 struct ExtentHint {
@@ -139,7 +159,8 @@ struct ArenaLaunch {
 constexpr uint32_t kBucketCount = 1024;
 constexpr uint32_t kBucketThreads = 1024;  // both launches; one payload per thread per grid stride
 constexpr size_t kCursorOff = 8192;        // the two cursor sets, in the extent scratch (2 x 4 KiB)
-static_assert((8 + 4 * kExtentMaxParts) * 8 <= kCursorOff && kCursorOff + 2 * 4 * kBucketCount <= kExtentScratchBytes,
+constexpr size_t kSplitCtrOff = kCursorOff + 2 * 4 * kBucketCount;  // 2 sets of 4 uint64 (split counters)
+static_assert((8 + 4 * kExtentMaxParts) * 8 <= kCursorOff && kSplitCtrOff + 2 * 32 <= kExtentScratchBytes,
               "extent scratch layout");
 // The ranges area (BucketArgs::ranges): the classes' bounds and two spare words
 constexpr uint32_t kRangeWords = 8;
@@ -149,8 +170,13 @@ struct BucketArgs {
   uint32_t* cursor;       // this call's set (zero on entry)
   uint32_t* cursor_next;  // the other set: zeroed by launch_bucket_place
   uint32_t* ranges;       // kRangeWords: [0, 1] = {begin, end} of the sorted list in desc, [2..5] empty
-  void* desc;             // uint4 {addr lo, addr hi, len, index} per non-empty payload
+  void* desc;             // uint4 {addr lo, addr hi, len, index} per non-empty payload (or segment)
   uint32_t* out;          // zero-length digests; null in update mode
+  // long payloads (launch_var_sorted): null split_slot = no splitting
+  unsigned long long* split_ctr;       // this call's counter set (zero on entry)
+  unsigned long long* split_ctr_next;  // the other set: zeroed by launch_bucket_place
+  uint32_t* split_slot;                // n words: a long payload's first slot, ~0 when it runs whole
+  uint4* split_rec;                    // kSplitRecCap records
 };
 unsigned bucket_grid(size_t n);  // blocks of both launches (= the extent partials: at most kExtentMaxParts)
 

@@ -26,13 +26,17 @@ def child():
 
     dev = torch.device("cuda", 0)
     lens, offs = bench.zipf_batch(0x5EED)
+    if os.environ.get("PROBE_BATCH") == "long":  # 256 payloads of 1 MiB and 20k of 4 KiB, 8 KiB gaps
+        rng = np.random.default_rng(9)
+        lens = rng.permutation(np.concatenate([np.full(256, 1 << 20), np.full(20000, 4096)]))
+        offs = np.concatenate([[0], np.cumsum(lens + 8192)[:-1]])
     if os.environ.get("PROBE_BATCH") == "small":  # 2M payloads of 16 B - 1 KiB, packed
         rng = np.random.default_rng(7)
         lens = rng.integers(16, 1025, 2 << 20)
         offs = np.concatenate([[0], np.cumsum(lens)[:-1]])
     g = torch.Generator(device=dev)
     g.manual_seed(4242)
-    data = torch.randint(0, 256, (int(lens.sum()),), dtype=torch.uint8, device=dev, generator=g)
+    data = torch.randint(0, 256, (int(offs[-1] + lens[-1]),), dtype=torch.uint8, device=dev, generator=g)
     d_off = torch.from_numpy(offs.astype(np.int64)).to(dev)
     d_len = torch.from_numpy(lens.astype(np.int32)).to(dev)
     annety_amd.set_var_path(os.environ.get("PROBE_PATH", "sorted"))  # auto: the arena for a dense batch
