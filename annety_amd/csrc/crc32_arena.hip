@@ -586,9 +586,12 @@ __device__ __forceinline__ uint32_t bucket_of(uint64_t a, uint32_t len) {
 }
 
 // A payload the sorted path may run as segments (crc32_kernels.h kSplitSeg): digest mode, longer than
-// kSplitMin, within the power table's reach.
+// kSplitMin; its segment size (a uint32 length is < 4096 big segments, within the power tables' reach).
 __device__ __forceinline__ bool split_eligible(const BucketArgs& bk, uint32_t l) {
-  return bk.split_slot && bk.out && l > kSplitMin && (l + (uint64_t)kSplitSeg - 1) / kSplitSeg <= kSplitMaxSegs;
+  return bk.split_slot && bk.out && l > kSplitMin;
+}
+__device__ __forceinline__ uint32_t split_seg(uint32_t l) {
+  return (uint64_t)l > (uint64_t)kSplitSeg * (kSplitMaxSegs - 1) ? kSplitSegBig : kSplitSeg;
 }
 
 // COUNT: step 1 of the counting sort (crc32_kernels.h BucketArgs) beside the extent.
@@ -617,23 +620,16 @@ __global__ __launch_bounds__(kExtentBlock) void crc32_extent_kernel(const uint64
       if (l) {
         const uint64_t a = (uint64_t)(uintptr_t)bk.base + o;
         bool split = false;
-        if (split_eligible(bk, (uint32_t)l)) {  // a long payload: claim segment slots and a record
-          const uint32_t S = (uint32_t)((l + kSplitSeg - 1) / kSplitSeg);
-          uint32_t slot = ~0u;
-          const unsigned long long s0 = atomicAdd(bk.split_ctr, (unsigned long long)S);
-          if (s0 + S <= kSplitSegCap) {
-            const unsigned long long r = atomicAdd(bk.split_ctr + 1, 1ull);
-            if (r < kSplitRecCap) {
-              bk.split_rec[r] = make_uint4((uint32_t)i, (uint32_t)s0, S, 0u);
-              slot = (uint32_t)s0;
-              split = true;
-            }
-          }
-          bk.split_slot[i] = slot;
-          if (split) {  // the first segment, then S - 1 of kSplitSeg bytes with the same alignment, one bucket
-            const uint32_t l0 = (uint32_t)l - (S - 1) * kSplitSeg;
+        if (split_eligible(bk, (uint32_t)l)) {  // a long payload: claim its extra descriptors
+          const uint32_t seg = split_seg((uint32_t)l);
+          const uint32_t S = (uint32_t)((l + seg - 1) / seg);
+          split = atomicAdd(bk.split_ctr, (unsigned long long)(S - 1)) + (S - 1) <= kSplitSegCap;
+          bk.split_slot[i] = split ? 1u : 0u;
+          if (split) {  // the first segment, then S - 1 of seg bytes with the same alignment, one bucket
+            bk.out[i] = ~0u;  // the segments xor into it
+            const uint32_t l0 = (uint32_t)l - (S - 1) * seg;
             atomicAdd(&h[bucket_of(a, l0)], 1u);
-            atomicAdd(&h[bucket_of(a + l0, kSplitSeg)], S - 1);
+            atomicAdd(&h[bucket_of(a + l0, seg)], S - 1);
           }
         }
         if (!split) atomicAdd(&h[bucket_of(a, (uint32_t)l)], 1u);
@@ -679,7 +675,7 @@ __global__ __launch_bounds__(kBucketThreads) void crc32_bucket_place(const uint6
   basep[t] = start + mine;
   if (blockIdx.x == 0) {
     bk.cursor_next[t] = 0u;
-    if (bk.split_ctr_next && t < 4) bk.split_ctr_next[t] = 0ull;
+    if (bk.split_ctr_next && t == 0) *bk.split_ctr_next = 0ull;
     // one class: every non-empty payload (crc32_kernels.hip var_class_w8); ranges[2..5] empty
     if (t == 0) bk.ranges[0] = 0u;
     if (t == kBucketCount - 1)
@@ -696,20 +692,20 @@ __global__ __launch_bounds__(kBucketThreads) void crc32_bucket_place(const uint6
     const uint32_t l = len[i];
     if (!l) continue;
     const uint64_t a = (uint64_t)(uintptr_t)bk.base + off[i];
-    if (split_eligible(bk, l)) {
-      const uint32_t slot = bk.split_slot[i];
-      if (slot != ~0u) {  // segments: the first (the remainder), then S - 1 of kSplitSeg bytes
-        const uint32_t S = (l + kSplitSeg - 1) / kSplitSeg, l0 = l - (S - 1) * kSplitSeg;
-        const uint32_t p0 = atomicAdd(&basep[bucket_of(a, l0)], 1u);
-        desc[p0] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), l0, kSegFlag | kSegFirst | slot);
-        const uint64_t a1 = a + l0;
-        const uint32_t pk = atomicAdd(&basep[bucket_of(a1, kSplitSeg)], S - 1);
-        for (uint32_t k = 1; k < S; k++) {
-          const uint64_t ak = a1 + (uint64_t)(k - 1) * kSplitSeg;
-          desc[pk + k - 1] = make_uint4((uint32_t)ak, (uint32_t)(ak >> 32), kSplitSeg, kSegFlag | (slot + k));
-        }
-        continue;
+    if (split_eligible(bk, l) && bk.split_slot[i]) {  // segments: the first (the remainder), then S - 1 of seg bytes
+      const uint32_t seg = split_seg(l), S = (l + seg - 1) / seg, l0 = l - (S - 1) * seg;
+      const uint32_t big = seg == kSplitSegBig ? kSegBig : 0u;
+      const uint32_t p0 = atomicAdd(&basep[bucket_of(a, l0)], 1u);
+      desc[p0] = make_uint4((uint32_t)a, (uint32_t)(a >> 32) | ((S - 1) << 16), l0,
+                            kSegFlag | kSegFirst | big | (uint32_t)i);
+      const uint64_t a1 = a + l0;
+      const uint32_t pk = atomicAdd(&basep[bucket_of(a1, seg)], S - 1);
+      for (uint32_t k = 1; k < S; k++) {
+        const uint64_t ak = a1 + (uint64_t)(k - 1) * seg;
+        desc[pk + k - 1] = make_uint4((uint32_t)ak, (uint32_t)(ak >> 32) | ((S - 1 - k) << 16), seg,
+                                      kSegFlag | big | (uint32_t)i);
       }
+      continue;
     }
     const uint32_t pos = atomicAdd(&basep[bucket_of(a, l)], 1u);  // LDS atomic: rank inside the block's slots
     desc[pos] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), l, (uint32_t)i);

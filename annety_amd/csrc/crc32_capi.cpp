@@ -543,13 +543,12 @@ int scratch_done(DeviceCtx& c, ScratchSlot* slot) {
 // crc32_kernels.h BucketArgs), then one launch per length class with its own lane-group width. Scratch:
 // the stream's slot (scratch_slot): the bucket cursors in the extent area, rows + ranges + descriptors
 // after it.
-// Layout after rows + ranges: descriptors (n, plus kSplitSegCap for split payloads' segments), split_slot (n
-// words, 16-byte padded), the split records, the segments' raw registers (crc32_kernels.h SortedSplit).
+// Layout after rows + ranges: descriptors (n, plus kSplitSegCap for long payloads' extra segments), then
+// split_slot (n words; crc32_kernels.h kSplitSeg).
 size_t sorted_desc_count(size_t n) { return n + kSplitSegCap; }
 size_t sorted_scratch_bytes(size_t n) {
   const size_t rows_words = (size_t)bucket_grid(n) * kBucketCount;
-  return (rows_words + kRangeWords) * sizeof(uint32_t) + 16 * sorted_desc_count(n) + ((4 * n + 15) & ~(size_t)15) +
-         16 * (size_t)kSplitRecCap + 4 * (size_t)kSplitSegCap;
+  return (rows_words + kRangeWords) * sizeof(uint32_t) + 16 * sorted_desc_count(n) + 4 * n;
 }
 int split_powers(DeviceCtx& c, uint64_t seg, const uint32_t** out);
 
@@ -564,16 +563,17 @@ bool sorted_fused() {
 int run_var_sorted_in(DeviceCtx& c, ScratchSlot* slot, const void* d_base, size_t n, const uint64_t* d_off,
                       const uint32_t* d_len, uint32_t* d_out, hipStream_t stream, bool update,
                       ExtentHint* record = nullptr, uint64_t seq = 0) {
-  if (n >= (size_t)kSegIndexMask) return ANNETY_CRC_EINVAL;  // descriptor indices keep bits 30-31 for segments
+  if (n > (size_t)kSegIndexMask) return ANNETY_CRC_EINVAL;  // descriptor indices keep bits 29-31 for segments
   uint32_t* cursors = reinterpret_cast<uint32_t*>(static_cast<char*>(slot->data.ptr) + kCursorOff);
   if (!slot->data.cursors_clean) {  // both cursor sets and both split counter sets (contiguous)
     const hipError_t z = hipMemsetAsync(cursors, 0, 2 * kBucketCount * sizeof(uint32_t) + 64, stream);
     if (z != hipSuccess) return hip_fail(z);
     slot->data.cursors_clean = true;
   }
-  const uint32_t* powers = nullptr;  // the split join's table (built once per device)
+  SortedSplit split{};  // the long payloads' power tables (built once per device)
   if (sorted_fused()) {
-    const int pr = split_powers(c, kSplitSeg, &powers);
+    int pr = split_powers(c, kSplitSeg, &split.powers);
+    if (pr == ANNETY_CRC_OK) pr = split_powers(c, kSplitSegBig, &split.powers_big);
     if (pr) return pr;
   }
   const size_t rows_words = (size_t)bucket_grid(n) * kBucketCount;
@@ -589,17 +589,10 @@ int run_var_sorted_in(DeviceCtx& c, ScratchSlot* slot, const void* d_base, size_
   bk.out = update ? nullptr : d_out;
   unsigned long long* sctr =
       reinterpret_cast<unsigned long long*>(static_cast<char*>(slot->data.ptr) + kSplitCtrOff);
-  char* after_desc = static_cast<char*>(bk.desc) + 16 * sorted_desc_count(n);
-  SortedSplit split{};
   if (sorted_fused()) {  // (the A/B per-class launches take no segments)
     bk.split_ctr = sctr + 4 * set;
     bk.split_ctr_next = sctr + 4 * (set ^ 1);
-    bk.split_slot = reinterpret_cast<uint32_t*>(after_desc);
-    bk.split_rec = reinterpret_cast<uint4*>(after_desc + ((4 * n + 15) & ~(size_t)15));
-    split.rec = bk.split_rec;
-    split.seg_crc = reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(bk.split_rec) + 16 * (size_t)kSplitRecCap);
-    split.ctr = bk.split_ctr;
-    split.powers = powers;
+    bk.split_slot = reinterpret_cast<uint32_t*>(static_cast<char*>(bk.desc) + 16 * sorted_desc_count(n));
   }
   uint32_t parts = 0;
   hipError_t e = launch_extent(d_off, d_len, n, slot->data.ptr, &parts, &bk, stream);

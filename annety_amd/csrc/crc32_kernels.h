@@ -64,24 +64,24 @@ struct VarLaunch {
 
 hipError_t launch_var(const VarLaunch& a, hipStream_t stream);
 // Long payloads on the sorted path (digest mode): a payload of more than kSplitMin bytes runs as end-aligned
-// segments of kSplitSeg bytes (the first takes the remainder), each a task of the sorted list, so that one long
-// payload no longer serialises kSplitSeg/1 KiB rounds per segment on one lane group. A segment's descriptor index
-// is kSegFlag | (kSegFirst if it is the payload's first) | its slot in seg_crc, which receives its raw register
-// (the first from the init, the others from 0); the launch's last block joins them,
-//   crc = ~xor_k shift_{(S-1-k) kSplitSeg}(seg_crc[slot + k])   (powers: crc32_capi.cpp split_powers).
-// Slots and records are claimed in the count step up to kSplitSegCap / kSplitRecCap per call; a payload that
-// finds none runs whole.
-constexpr uint32_t kSplitSeg = 65536;
-constexpr uint32_t kSplitMin = 2 * kSplitSeg;
-constexpr uint32_t kSplitMaxSegs = 16384;      // the power table's reach (crc32_capi.cpp kMaxSegs)
-constexpr uint32_t kSplitSegCap = 1u << 18;    // segment slots per call
-constexpr uint32_t kSplitRecCap = 1u << 15;    // split payloads per call
-constexpr uint32_t kSegFlag = 0x80000000u, kSegFirst = 0x40000000u, kSegIndexMask = 0x3FFFFFFFu;
+// segments of kSplitSeg bytes (kSplitSegBig past kSplitSeg * kSplitMaxSegs; the first segment takes the
+// remainder), each a task of the sorted list, so that one long payload no longer serialises its rounds on one lane
+// group. A segment's descriptor carries kSegFlag (| kSegFirst for the first, | kSegBig) | the payload's index in
+// .w and m = the segments after it in bits 16-31 of .y (addresses are 48-bit). The group that finishes a segment
+// applies shift_{m seg} to its raw register (the first from the init, the others from 0) from the power table and
+// xors it into out[payload], which the count step preset to ~0, so the digest = ~xor_k shift_{m_k seg}(raw_k)
+// needs no join. Extra descriptors are claimed in the count step up to kSplitSegCap per call; a payload that finds
+// none runs whole.
+constexpr uint32_t kSplitSeg = 16384;
+constexpr uint32_t kSplitSegBig = 1u << 20;
+constexpr uint32_t kSplitMin = 131072;
+constexpr uint32_t kSplitMaxSegs = 16384;      // the power tables' reach (crc32_capi.cpp kMaxSegs)
+constexpr uint32_t kSplitSegCap = 1u << 18;    // extra descriptors per call
+constexpr uint32_t kSegFlag = 0x80000000u, kSegFirst = 0x40000000u, kSegBig = 0x20000000u,
+                   kSegIndexMask = 0x1FFFFFFFu;
 struct SortedSplit {
-  uint32_t* seg_crc;           // kSplitSegCap words
-  const uint4* rec;            // kSplitRecCap records {payload, first slot, segments, 0}
-  unsigned long long* ctr;     // this call's counters: [0] slots, [1] records, [2] finished blocks
-  const uint32_t* powers;      // powers[(m-1)*32 + bit] = shift_{m*kSplitSeg}(1 << bit)
+  const uint32_t* powers;      // powers[(m-1)*32 + bit] = shift_{m*kSplitSeg}(1 << bit), m = 1..kSplitMaxSegs-1
+  const uint32_t* powers_big;  // the same for kSplitSegBig
 };
 // The sorted path in one launch (a.range[0..1] = the sorted list's bounds in a.desc); img_w8 = the w8 image
 // (kW8ImgBytes, crc32_math.h); a.group, a.img_group and a.img_unshift are ignored.

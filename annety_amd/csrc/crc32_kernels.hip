@@ -647,12 +647,14 @@ __global__ __launch_bounds__(kBlock) void crc32_var_kernel(const uint8_t* __rest
 struct W8Task {
   uint64_t a0;  // address of the payload's first line (128-aligned)
   uint32_t lead, te, h, R, p, state;
-  uint32_t seg;  // 0: a payload (p = its index); 1: a split payload's first segment, 2: a later one (p = slot)
+  // 0: a payload; else a split payload's segment (crc32_kernels.h kSplitSeg): bit 0 its first, bit 1 a later one,
+  // bit 2 big segments, bits 16-31 m = the segments after it (p = the payload's index either way)
+  uint32_t seg;
   bool valid;
 };
 __device__ __forceinline__ W8Task decode_w8(uint4 d, bool valid) {
   W8Task k;
-  const uint64_t a = ((uint64_t)d.y << 32) | d.x;
+  const uint64_t a = ((uint64_t)(d.y & 0xFFFFu) << 32) | d.x;  // (48-bit addresses; a segment's m above them)
   const uint64_t e = a + d.z;  // d.z > 0
   const uint64_t L0 = a >> 7;
   const uint32_t nl = (uint32_t)(((e - 1) >> 7) - L0 + 1);
@@ -661,7 +663,8 @@ __device__ __forceinline__ W8Task decode_w8(uint4 d, bool valid) {
   k.te = (uint32_t)(((e - 1) & 127) + 1);
   k.h = ((nl - 1) & 7u) + 1;
   k.R = ((nl - k.h) >> 3) + 1;
-  k.seg = (d.w & kSegFlag) ? ((d.w & kSegFirst) ? 1u : 2u) : 0u;
+  k.seg = (d.w & kSegFlag) ? (((d.w & kSegFirst) ? 1u : 2u) | ((d.w & kSegBig) ? 4u : 0u) | (d.y & 0xFFFF0000u))
+                           : 0u;
   k.p = k.seg ? d.w & kSegIndexMask : d.w;
   k.state = 0;
   k.valid = valid;
@@ -678,7 +681,7 @@ template <bool UPD, int PROBE = 0>
 __device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restrict__ base,
                                              const uint4* __restrict__ desc, const uint32_t* __restrict__ range,
                                              const uint4* __restrict__ img_slice, const uint4* __restrict__ img_w8,
-                                             uint32_t* __restrict__ out, uint32_t* __restrict__ seg_crc) {
+                                             uint32_t* __restrict__ out, const SortedSplit& split) {
   constexpr int G = 8;
   const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
   const uint32_t l = threadIdx.x & 63, l3 = (l >> 3) & 1, j = l & 7;
@@ -846,7 +849,7 @@ __device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restr
     fold(v);
     // head round: line 0's register gains the init as a register at the payload start, shift_{128-lead}(init)
     if (__builtin_amdgcn_ballot_w64(head) != 0) {
-      if (head && j == up && cur.seg != 2) {  // (a split payload's later segments start from register 0)
+      if (head && j == up && (cur.seg & 2u) == 0) {  // (a split payload's later segments start from register 0)
         if constexpr (UPD) {
           uint32_t x = w8_unshift(cur.state, cur.lead, lds);                       // shift_{-lead}
           s ^= byte_map64(byte_map64(x, lds, kLdsW8HalfOff), lds, kLdsW8HalfOff);  // shift_128
@@ -860,10 +863,19 @@ __device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restr
       if (last && j == G - 1) {
         const uint32_t over = 128 - cur.te;  // the last line's bytes past the payload end (zeroed above)
         const uint32_t u = over ? w8_unshift(t, over, lds) : t;
-        if (cur.seg)
-          seg_crc[cur.p] = u;  // a segment's raw register (joined at the launch's end)
-        else
+        if (cur.seg) {  // a segment: shift_{m seg}(raw) into the payload's digest (preset to ~0)
+          const uint32_t m = cur.seg >> 16;
+          uint32_t x = u;
+          if (m) {
+            const uint32_t* P = ((cur.seg & 4u) ? split.powers_big : split.powers) + (size_t)(m - 1) * 32;
+            x = 0;
+#pragma unroll
+            for (int b = 0; b < 32; b++) x ^= P[b] & (0u - ((u >> b) & 1u));
+          }
+          atomicXor(out + cur.p, x);
+        } else {
           out[cur.p] = UPD ? u : ~u;
+        }
       }
       s = last ? 0u : s;
     }
@@ -916,44 +928,7 @@ __global__ __launch_bounds__(kW8Block) void crc32_var_sorted_kernel(const uint8_
                                                                   uint32_t* __restrict__ out, SortedSplit split) {
   __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsW8TotalBytes / 16];
   static_assert(kW8Block % 64 == 0 && kW8Block / 64 <= kW8MaxWaves, "the claim rings hold one ring per wave");
-  var_class_w8<UPD, PROBE>(lds4, base, desc, ranges, img_slice, img_w8, out, split.seg_crc);
-  if (UPD || !split.ctr) return;  // (update mode never splits)
-  // no split payload in this call (the count step finished before this launch): no fences, no join. An
-  // agent-scope fence in every wave cost 50 us per config-3 call.
-  if (__hip_atomic_load(split.ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0) return;
-  // The last block to finish joins the split payloads' segments (crc32_kernels.h SortedSplit). Every thread
-  // makes its segment stores visible at agent scope before its block counts itself done.
-  __threadfence();
-  __syncthreads();
-  uint32_t* flag = reinterpret_cast<uint32_t*>(lds4) + kLdsW8CounterOff / 4 + 2;  // (the set counter's spare word)
-  if (threadIdx.x == 0)
-    *flag = atomicAdd(split.ctr + 2, 1ull) == (unsigned long long)gridDim.x - 1 ? 1u : 0u;
-  __syncthreads();
-  if (*flag == 0) return;
-  __threadfence();  // acquire: the other blocks' segment stores
-  const unsigned long long nrec_all = __hip_atomic_load(split.ctr + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  const uint32_t nrec = nrec_all < kSplitRecCap ? (uint32_t)nrec_all : kSplitRecCap;
-  const uint32_t lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (uint32_t r = wave; r < nrec; r += kW8Block / 64) {
-    const uint4 rec = split.rec[r];  // {payload, first slot, segments}
-    uint32_t acc = 0;
-    for (uint32_t k = lane; k < rec.z; k += 64) {
-      const uint32_t c = __builtin_nontemporal_load(split.seg_crc + rec.y + k);
-      const uint32_t m = rec.z - 1 - k;
-      if (m == 0) {
-        acc ^= c;
-      } else {
-        const uint32_t* P = split.powers + (size_t)(m - 1) * 32;
-        uint32_t x = 0;
-#pragma unroll
-        for (int b = 0; b < 32; b++) x ^= P[b] & (0u - ((c >> b) & 1u));
-        acc ^= x;
-      }
-    }
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) acc ^= __shfl_xor(acc, o, 64);
-    if (lane == 0) out[rec.x] = ~acc;
-  }
+  var_class_w8<UPD, PROBE>(lds4, base, desc, ranges, img_slice, img_w8, out, split);
 }
 
 // ---- long payloads: segments + CRC combine ----

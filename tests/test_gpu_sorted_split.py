@@ -1,8 +1,9 @@
 """Long payloads on the length-sorted path (crc32_kernels.h kSplitSeg): a payload of more than 128 KiB runs as
-end-aligned 64 KiB segments (the first takes the remainder), each a task of the sorted list, and the launch's last
-block joins the segments' raw registers with the power table. Digests against the oracle at the edges: lengths
-just above the split threshold (a first segment of 1 byte), whole multiples of the segment, every start offset
-class, payloads of several MiB, long payloads mixed with many short ones, and update mode (never split)."""
+end-aligned 16 KiB segments (1 MiB past 256 MiB; the first takes the remainder), each a task of the sorted list,
+whose group xors shift_{m seg}(its raw register) into the payload's digest. Digests against the oracle at the
+edges: lengths just above the split threshold (a first segment of 1 byte), whole multiples of the segment, every
+start offset class, payloads of several MiB and one past 256 MiB, long payloads mixed with many short ones, and
+update mode (never split)."""
 import numpy as np
 import pytest
 
@@ -10,7 +11,8 @@ import oracle
 
 pytestmark = pytest.mark.gpu
 
-SEG = 65536
+SEG = 16384
+MIN = 131072  # kSplitMin
 
 
 def _run(gpu, lens, seed, path="sorted", gap=9000):
@@ -41,23 +43,28 @@ def _run(gpu, lens, seed, path="sorted", gap=9000):
 
 
 def test_split_edges(gpu):
-    lens = [2 * SEG + 1, 2 * SEG, 2 * SEG + 15, 3 * SEG, 3 * SEG + 16, 5 * SEG - 1, 7 * SEG + 129, 200000,
-            (1 << 20) + 3, 3 * (1 << 20) + 13, 4096, 1, 0, 127, 128, 129, SEG]
+    lens = [MIN + 1, MIN, MIN + 15, MIN + SEG, MIN + SEG + 16, 12 * SEG - 1, 13 * SEG + 129, 200000,
+            (1 << 20) + 3, 3 * (1 << 20) + 13, 4096, 1, 0, 127, 128, 129, SEG, 65536]
     kernels = _run(gpu, lens, 1)
     assert "crc32_var_sorted_kernel" in kernels
 
 
 def test_split_many_long_among_short(gpu):
     rng = np.random.default_rng(2)
-    lens = np.concatenate([rng.integers(0, 5000, 3000), rng.integers(2 * SEG + 1, 12 * SEG, 60),
+    lens = np.concatenate([rng.integers(0, 5000, 3000), rng.integers(MIN + 1, 50 * SEG, 60),
                            np.full(4, 16 << 20)])
     _run(gpu, rng.permutation(lens), 3)
 
 
 def test_split_every_remainder_and_alignment(gpu):
     # the first segment's length runs through 1..128 and every start offset class of a line
-    lens = [2 * SEG + r for r in range(1, 129)] + [4 * SEG + 64 * r + 1 for r in range(0, 32)]
+    lens = [MIN + r for r in range(1, 129)] + [MIN + 2 * SEG + 64 * r + 1 for r in range(0, 32)]
     _run(gpu, lens, 4, gap=4100)
+
+
+def test_split_big_segments(gpu):
+    # past kSplitSeg * (kSplitMaxSegs - 1) bytes the segments are 1 MiB
+    _run(gpu, [300 * (1 << 20) + 77, 5000, (1 << 20) + 1], 7, gap=5000)
 
 
 def test_split_through_the_automatic_path(gpu):
@@ -73,7 +80,7 @@ def test_update_mode_long_payloads(gpu):
     import annety_amd
 
     rng = np.random.default_rng(6)
-    lens = np.concatenate([rng.integers(2 * SEG + 1, 6 * SEG, 12), rng.integers(0, 3000, 200)]).astype(np.int64)
+    lens = np.concatenate([rng.integers(MIN + 1, 24 * SEG, 12), rng.integers(0, 3000, 200)]).astype(np.int64)
     offs = np.concatenate([[0], np.cumsum(lens + 5000)[:-1]]).astype(np.int64)
     data = oracle.lcg_bytes(int(offs[-1] + lens[-1]) + 256, 6)
     d = torch.from_numpy(data.copy()).to(gpu)
