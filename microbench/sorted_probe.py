@@ -30,6 +30,9 @@ def child():
         rng = np.random.default_rng(9)
         lens = rng.permutation(np.concatenate([np.full(256, 1 << 20), np.full(20000, 4096)]))
         offs = np.concatenate([[0], np.cumsum(lens + 8192)[:-1]])
+    if os.environ.get("PROBE_BATCH") == "huge":  # 16 payloads of 64 MiB, packed (1 GiB)
+        lens = np.full(16, 64 << 20)
+        offs = np.concatenate([[0], np.cumsum(lens)[:-1]])
     if os.environ.get("PROBE_BATCH") == "small":  # 2M payloads of 16 B - 1 KiB, packed
         rng = np.random.default_rng(7)
         lens = rng.integers(16, 1025, 2 << 20)
@@ -60,7 +63,7 @@ def main():
     if os.environ.get("SORTED_PROBE_CHILD"):
         return child()
     settings = sys.argv[1:] or ["0", "1", "2"]
-    lib = os.path.join(ROOT, "microbench", "libannety_crc_ab.so")
+    lib = os.environ.get("PROBE_LIB") or os.path.join(ROOT, "microbench", "libannety_crc_ab.so")
     for rep in range(2):
         for pr in settings:
             env = dict(os.environ, SORTED_PROBE_CHILD="1", ANNETY_CRC_LIB=lib, ANNETY_CRC_W8_PROBE=pr,
