@@ -273,6 +273,9 @@ struct Scratch {
   // the sorted path's bucket cursors (crc32_kernels.h BucketArgs): set (sorts & 1) is this call's
   uint64_t sorts = 0;
   bool cursors_clean = false;  // both sets zero (false after an allocation or a failed sort)
+  // the fused encode's long-frame counters (crc32_kernels.h EncLong): set (encodes & 1) is this call's
+  uint64_t encodes = 0;
+  bool enc_clean = false;  // both sets zero (false after an allocation or a failed encode)
   struct Key {
     const void *base, *off, *len;
     size_t n;
@@ -524,6 +527,7 @@ int scratch_slot(DeviceCtx& c, hipStream_t stream, size_t bytes, ScratchSlot** o
     HIP_TRY(hipMallocAsync(&d.ptr, kExtentScratchBytes + bytes, stream));
     d.bytes = bytes;
     d.cursors_clean = false;
+    d.enc_clean = false;
   }
   *out = slot;
   return ANNETY_CRC_OK;
@@ -1298,10 +1302,53 @@ static int encode_batch(const FrameRules& r, const void* d_src, const uint64_t* 
   int rc = stream_ctx(static_cast<hipStream_t>(stream), &c);
   if (rc) return rc;
   hipStream_t s = static_cast<hipStream_t>(stream);
-  // one pass: each payload read once, its frame (header, copy, CRC trailer) written once (crc32_frames.hip)
-  HIP_TRY(launch_lhc_encode_fused(d_src, d_src_off, d_len, n, r.T, r.enc_min, r.enc_max, d_dst, d_frame_off, c->d_zero,
-                                  c->d_slice, c->d_w8, grid_cus(*c), s));
-  return ANNETY_CRC_OK;
+  SortedSplit split{};  // the long frames' segment power tables (built once per device)
+  rc = split_powers(*c, kSplitSeg, &split.powers);
+  if (rc == ANNETY_CRC_OK) rc = split_powers(*c, kSplitSegBig, &split.powers_big);
+  if (rc) return rc;
+  std::lock_guard<std::mutex> lk(c->arena_mu);
+  ScratchSlot* slot = nullptr;
+  if ((rc = scratch_slot(*c, s, kEncLongScratchBytes, &slot))) return rc;
+  Scratch& d = slot->data;
+  char* ctrs = static_cast<char*>(d.ptr) + kEncCtrOff;
+  if (!d.enc_clean) {  // both counter sets
+    const hipError_t z = hipMemsetAsync(ctrs, 0, 32, s);
+    if (z != hipSuccess) return hip_fail(z);
+    d.enc_clean = true;
+  }
+  const uint32_t set = (uint32_t)(d.encodes & 1);
+  EncLong lg{};
+  lg.ctr = reinterpret_cast<unsigned long long*>(ctrs + 16 * set + 8);
+  lg.ctr_next = reinterpret_cast<unsigned long long*>(ctrs + 16 * (set ^ 1) + 8);
+  char* scratch = path_scratch(slot);
+  lg.digest = reinterpret_cast<uint32_t*>(scratch);
+  lg.entry = lg.digest + kEncLongCap;
+  lg.desc = scratch + 8 * kEncLongCap;
+  lg.seg_dst = reinterpret_cast<uint64_t*>(scratch + 8 * kEncLongCap + 16 * kEncLongSegCap);
+  // one pass: each payload read once, its frame (header, copy, CRC trailer) written once (crc32_frames.hip); the
+  // long frames it hands over: their digests on the sorted kernel (segments), then their copy, headers and trailers
+  hipError_t e = launch_lhc_encode_fused(d_src, d_src_off, d_len, n, r.T, r.enc_min, r.enc_max, d_dst, d_frame_off,
+                                         c->d_zero, c->d_slice, c->d_w8, lg, grid_cus(*c), s);
+  if (e == hipSuccess) {
+    VarLaunch a{};
+    a.base = d_src;
+    a.n = kEncLongCap;
+    a.desc = lg.desc;
+    a.range = reinterpret_cast<const uint32_t*>(lg.ctr) - 1;  // {0, segments}
+    a.img_slice = c->d_slice;
+    a.img_unshift = c->d_unshift;
+    a.out = lg.digest;
+    a.max_blocks = grid_cus(*c);
+    e = launch_var_sorted(a, c->d_w8, split, s);
+  }
+  if (e == hipSuccess) e = launch_lhc_encode_long(d_len, r.T, d_dst, d_frame_off, lg, grid_cus(*c), s);
+  if (e != hipSuccess) {
+    d.enc_clean = false;  // the next call zeroes both sets first
+    (void)scratch_done(*c, slot);
+    return hip_fail(e);
+  }
+  d.encodes++;
+  return scratch_done(*c, slot);
 }
 
 int annety_lhc_encode_batch(const void* d_src, const uint64_t* d_src_off, const uint32_t* d_len, size_t n,

@@ -76,6 +76,171 @@ __device__ __forceinline__ uint64_t encw_round(const EncW& k, uint32_t r) {
   return k.a0() + (r == 0 ? 0ull : (uint64_t)k.h * 128u + (uint64_t)(r - 1) * 1024u);
 }
 
+// The long path's claim (crc32_kernels.h EncLong), by a frame's lane group (its 8 lanes alike; want false: no
+// claim). Lane 0 takes an entry and the frame's S segment descriptors from the counter (a compare-and-swap, so a
+// claim past either cap takes nothing); the group writes the descriptors in crc32_var_sorted_kernel's segment
+// format (crc32_arena.hip crc32_bucket_place: end-aligned, the first takes the remainder, m = segments after it)
+// and the entry, and presets the digest the segments xor into. Returns whether the frame was taken.
+__device__ __forceinline__ bool enc_hand_over(const EncLong& lg, uint64_t A, uint64_t Dp, uint32_t L, uint32_t t,
+                                              bool want, uint32_t l) {
+  const uint32_t seg = (uint64_t)L > (uint64_t)kSplitSeg * (kSplitMaxSegs - 1) ? kSplitSegBig : kSplitSeg;
+  const uint32_t S = (uint32_t)(((uint64_t)L + seg - 1) / seg);
+  uint32_t e = ~0u, b = 0;
+  if (want && (l & 7u) == 0) {
+    unsigned long long old = __hip_atomic_load(lg.ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    while (true) {
+      const uint32_t segs = (uint32_t)old, ents = (uint32_t)(old >> 32);
+      if (ents >= kEncLongCap || (uint64_t)segs + S > kEncLongSegCap) break;
+      const unsigned long long prev = atomicCAS(lg.ctr, old, old + ((1ull << 32) | S));
+      if (prev == old) {
+        e = ents;
+        b = segs;
+        break;
+      }
+      old = prev;
+    }
+  }
+  e = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * (l & ~7u)), (int)e);
+  b = (uint32_t)__builtin_amdgcn_ds_bpermute((int)(4 * (l & ~7u)), (int)b);
+  if (!want || e == ~0u) return false;
+  const uint32_t l0 = L - (S - 1) * seg;
+  const uint32_t big = seg == kSplitSegBig ? kSegBig : 0u;
+  uint4* desc = static_cast<uint4*>(lg.desc);
+  for (uint32_t k = l & 7u; k < S; k += 8) {
+    const uint64_t ak = k == 0 ? A : A + l0 + (uint64_t)(k - 1) * seg;
+    desc[b + k] = make_uint4((uint32_t)ak, (uint32_t)(ak >> 32) | ((S - 1 - k) << 16), k == 0 ? l0 : seg,
+                             kSegFlag | (k == 0 ? kSegFirst : 0u) | big | e);
+    lg.seg_dst[b + k] = Dp + (ak - A);
+  }
+  if ((l & 7u) == 0) {
+    lg.entry[e] = t;
+    lg.digest[e] = ~0u;
+  }
+  return true;
+}
+
+// The frames the fused kernel handed over (digests from crc32_var_sorted_kernel): the copy runs over the segment
+// descriptors, a block per segment, two segments per block in flight (their descriptors, destinations and 2 x 512
+// chunks loaded before any store). The destination is cut into aligned 16-byte chunks of the FRAME: a segment owns
+// the chunks that start inside it (the first segment also the one holding the payload's first byte), so a chunk
+// that straddles two segments is whole, loaded from two aligned source chunks and stored once after a byte funnel,
+// and only the payload's first and last chunks are partial (their bytes stored one by one). Thread e < frames
+// stores frame e's header and trailer (as the fused kernel does). Block 0 zeroes the next call's counter.
+constexpr int kEncLongBlock = 512;  // (2 blocks per CU: at 1024 lanes the four chunks in flight spill)
+constexpr int kEncLongIlp = 2;  // segments per block in flight
+constexpr int kEncLongPer = 2;  // chunks per thread and segment in flight (a 16 KiB segment: 1024 chunks)
+struct EncSeg {
+  uint64_t lo;      // the segment's first owned chunk
+  uint64_t nc;      // owned chunks
+  uint64_t Df, Ef;  // the payload's destination bounds where the segment holds them (else 0 / ~0)
+  uint64_t delta;   // destination - source
+  uint64_t safe;    // the aligned source chunk holding the segment's first byte (the address of loads not used)
+};
+struct EncChunk {
+  uint64_t dc;  // destination chunk address
+  uint4 x0, x1;
+  uint32_t o;   // source byte offset in x0:x1
+  bool whole, on;
+};
+__device__ __forceinline__ void enc_chunk_load(EncChunk& ch, const EncSeg& g, uint64_t q, bool on) {
+  ch.dc = g.lo + 16 * q;
+  ch.on = on && q < g.nc;
+  ch.whole = ch.on && ch.dc >= g.Df && ch.dc + 16 <= g.Ef;
+  const uint64_t sp = ch.dc - g.delta, sa = sp & ~15ull;
+  ch.o = (uint32_t)sp & 15u;
+  // unconditional loads (a select of the second load made the compiler wait for the first): a chunk that is not
+  // whole loads the segment's first source chunk; the second load is the next source chunk when o > 0 (it holds a
+  // payload byte then), else the first again. Nontemporal: every byte is read once, by one or two neighbouring lanes.
+  const uint64_t l0 = ch.whole ? sa : g.safe;
+  ch.x0 = gload16_nt(l0, 0);
+  ch.x1 = gload16_nt(l0, ch.whole && ch.o ? 16u : 0u);
+}
+__device__ __forceinline__ void enc_chunk_store(const EncChunk& ch, const EncSeg& g) {
+  if (ch.whole) {
+    const uint32_t w[8] = {ch.x0.x, ch.x0.y, ch.x0.z, ch.x0.w, ch.x1.x, ch.x1.y, ch.x1.z, ch.x1.w};
+    const uint32_t qd = ch.o >> 2, sh = ch.o & 3u;
+    uint32_t y[5];
+#pragma unroll
+    for (int k = 0; k < 5; k++) y[k] = qd == 0 ? w[k] : (qd == 1 ? w[k + 1] : (qd == 2 ? w[k + 2] : w[k + 3]));
+    gstore16_nt(ch.dc, make_uint4(__builtin_amdgcn_alignbyte(y[1], y[0], sh), __builtin_amdgcn_alignbyte(y[2], y[1], sh),
+                                  __builtin_amdgcn_alignbyte(y[3], y[2], sh), __builtin_amdgcn_alignbyte(y[4], y[3], sh)));
+  } else if (ch.on) {
+    // the payload's first or last chunk: the <= 2 aligned source chunks holding its payload bytes (both hold one,
+    // so no load leaves the payload's chunks), then the bytes one by one
+    const uint64_t b0 = ch.dc > g.Df ? ch.dc : g.Df, b1 = ch.dc + 16 < g.Ef ? ch.dc + 16 : g.Ef;
+    const uint64_t g0 = (b0 - g.delta) & ~15ull, g1 = (b1 - 1 - g.delta) & ~15ull;
+    const uint4 y0 = gload16(g0), y1 = g1 != g0 ? gload16(g1) : y0;
+    for (uint64_t x = b0; x < b1; x++) {
+      const uint32_t i = (uint32_t)(x - g.delta - g0), q = (i >> 2) & 3u;
+      const uint4 y = i < 16 ? y0 : y1;
+      const uint32_t wd = q == 0 ? y.x : (q == 1 ? y.y : (q == 2 ? y.z : y.w));
+      gstore1(x, wd >> (8 * (i & 3u)));
+    }
+  }
+}
+__global__ __launch_bounds__(kEncLongBlock) void lhc_encode_long_kernel(const uint32_t* __restrict__ len, int T,
+                                                                     uint8_t* __restrict__ dst,
+                                                                     const uint64_t* __restrict__ dst_off,
+                                                                     EncLong lg) {
+  const unsigned long long cv = *lg.ctr;
+  const uint32_t ents = min((uint32_t)(cv >> 32), kEncLongCap), segs = min((uint32_t)cv, kEncLongSegCap);
+  if (blockIdx.x == 0 && threadIdx.x == 0) *lg.ctr_next = 0ull;
+  const uint32_t c = threadIdx.x, nb = gridDim.x;
+  const uint4* desc = static_cast<const uint4*>(lg.desc);
+  for (uint32_t k0 = blockIdx.x; k0 < segs; k0 += kEncLongIlp * nb) {
+    EncSeg g[kEncLongIlp];
+    bool on[kEncLongIlp];
+#pragma unroll
+    for (int u = 0; u < kEncLongIlp; u++) {
+      const uint32_t k = k0 + u * nb;
+      on[u] = k < segs;
+      const uint32_t kk = on[u] ? k : k0;
+      const uint4 d = desc[kk];
+      const uint64_t a = ((uint64_t)(d.y & 0xFFFFu) << 32) | d.x;
+      const uint64_t D0 = lg.seg_dst[kk], E0 = D0 + d.z;
+      const bool first = (d.w & kSegFirst) != 0, last = (d.y >> 16) == 0;
+      g[u].lo = first ? D0 & ~15ull : (D0 + 15) & ~15ull;
+      g[u].nc = ((((E0 - 1) & ~15ull) - g[u].lo) >> 4) + 1;
+      g[u].Df = first ? D0 : 0ull;
+      g[u].Ef = last ? E0 : ~0ull;
+      g[u].delta = D0 - a;
+      g[u].safe = a & ~15ull;
+    }
+    EncChunk ch[kEncLongIlp][kEncLongPer];
+#pragma unroll
+    for (int u = 0; u < kEncLongIlp; u++)
+#pragma unroll
+      for (int v = 0; v < kEncLongPer; v++) enc_chunk_load(ch[u][v], g[u], c + v * kEncLongBlock, on[u]);
+#pragma unroll
+    for (int u = 0; u < kEncLongIlp; u++)
+#pragma unroll
+      for (int v = 0; v < kEncLongPer; v++) enc_chunk_store(ch[u][v], g[u]);
+    // the rest of each segment's chunks (the last one of a 16 KiB segment whose destination is not aligned, the
+    // 1 MiB segments')
+#pragma unroll
+    for (int u = 0; u < kEncLongIlp; u++) {
+      if (!on[u]) continue;
+      for (uint64_t q = c + kEncLongPer * kEncLongBlock; q < g[u].nc; q += kEncLongBlock) {
+        EncChunk x;
+        enc_chunk_load(x, g[u], q, true);
+        enc_chunk_store(x, g[u]);
+      }
+    }
+  }
+  const uint64_t gt = blockIdx.x * (uint64_t)kEncLongBlock + threadIdx.x, gs = (uint64_t)gridDim.x * kEncLongBlock;
+  for (uint64_t e = gt; e < ents; e += gs) {
+    const uint32_t i = lg.entry[e];
+    const uint32_t L = len[i];
+    const uint64_t D = (uint64_t)(uintptr_t)(dst + dst_off[i]) + (uint32_t)T;
+    gstore4(D + L, __builtin_bswap32(lg.digest[e]));  // the trailer, big-endian
+    const uint64_t hdr = (uint64_t)L + 4, hp = D - (uint64_t)T;
+    if (T == 1) gstore1(hp, (uint32_t)hdr);
+    else if (T == 2) gstore2(hp, __builtin_bswap32((uint32_t)hdr) >> 16);
+    else if (T == 4) gstore4(hp, __builtin_bswap32((uint32_t)hdr));
+    else gstore8(hp, __builtin_bswap64(hdr));
+  }
+}
+
 // 512 lanes per block (2 waves per SIMD over the one LDS image). 768 lanes (3 per SIMD) measured 0.588 against
 // 0.637 ms on chat frames and 0.676 against 0.682 on mixed ones, but spill (the kernel needs ~175 VGPRs of 168).
 constexpr int kEncBlock = 512;
@@ -91,7 +256,8 @@ __global__ __launch_bounds__(kEncBlock) void lhc_encode_fused_kernel(const uint8
                                                                   const uint64_t* __restrict__ dst_off,
                                                                   uint64_t zero_line,
                                                                   const uint4* __restrict__ img_slice,
-                                                                  const uint4* __restrict__ img_w8) {
+                                                                  const uint4* __restrict__ img_w8,
+                                                                  EncLong lg) {
   constexpr int G = 8;
   __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsW8ImageBytes / 16];
   const uint32_t* lds = reinterpret_cast<const uint32_t*>(lds4);
@@ -109,8 +275,14 @@ __global__ __launch_bounds__(kEncBlock) void lhc_encode_fused_kernel(const uint8
     ln = len[tc];
     fo = dst_off[tc];
   };
+  // a frame of more than kEncLongMin bytes that finds room on the long path (crc32_kernels.h EncLong) is handed
+  // over there and idles here (decoded as an empty frame); called with the group's 8 lanes alike
   auto dec = [&](size_t t, uint64_t so, uint32_t ln, uint64_t fo) __attribute__((always_inline)) {
-    return decode_encw(src, dst, so, ln, fo, T, enc_min, enc_max, t < n, zero_line);
+    EncW d = decode_encw(src, dst, so, ln, fo, T, enc_min, enc_max, t < n, zero_line);
+    const bool want = d.valid && d.L > kEncLongMin;
+    if (__builtin_amdgcn_ballot_w64(want) != 0 && enc_hand_over(lg, d.A, d.Dp, d.L, (uint32_t)t, want, l))
+      d = decode_encw(src, dst, so, 0u, fo, T, enc_min, enc_max, t < n, zero_line);
+    return d;
   };
   // Load i reads the round of group m(i) = (i >> 2) + 2 (i & 1) + 4 ((i >> 1) & 1) (var_class_w8's order); a lane's
   // chunk past the group's last one re-reads that one (lim: the last chunk's offset in the round)
@@ -329,7 +501,7 @@ hipError_t launch_lhc_compare(const void* stream_base, const uint64_t* off, cons
 hipError_t launch_lhc_encode_fused(const void* src, const uint64_t* src_off, const uint32_t* len, size_t n, int T,
                                    int64_t enc_min, int64_t enc_max, void* dst, const uint64_t* dst_off,
                                    const void* zero_line, const void* img_slice, const void* img_w8,
-                                   size_t max_blocks, hipStream_t stream) {
+                                   const EncLong& lg, size_t max_blocks, hipStream_t stream) {
   if (n == 0) return hipSuccess;
   const size_t want = (n * 8 + kEncBlock - 1) / kEncBlock;
   const unsigned blocks = (unsigned)std::max<size_t>(1, std::min(max_blocks, want));
@@ -338,7 +510,7 @@ hipError_t launch_lhc_encode_fused(const void* src, const uint64_t* src_off, con
   hipLaunchKernelGGL(lhc_encode_fused_kernel<P>, dim3(blocks), dim3(kEncBlock), 0, stream,                             \
                      static_cast<const uint8_t*>(src), src_off, len, n, T, enc_min, enc_max, static_cast<uint8_t*>(dst), \
                      dst_off, (uint64_t)(uintptr_t)zero_line, static_cast<const uint4*>(img_slice),                 \
-                     static_cast<const uint4*>(img_w8))
+                     static_cast<const uint4*>(img_w8), lg)
 #ifdef ANNETY_CRC_AB
   static const int probe = ANNETY_AB_KNOB("ANNETY_CRC_ENC_PROBE", 0);
   if (probe == 1) ANNETY_ENC_LAUNCH(1);
@@ -352,6 +524,14 @@ hipError_t launch_lhc_encode_fused(const void* src, const uint64_t* src_off, con
   ANNETY_ENC_LAUNCH(0);
 #endif
 #undef ANNETY_ENC_LAUNCH
+  return hipGetLastError();
+}
+
+hipError_t launch_lhc_encode_long(const uint32_t* len, int T, void* dst, const uint64_t* dst_off, const EncLong& lg,
+                                  size_t max_blocks, hipStream_t stream) {
+  note_kernel("lhc_encode_long_kernel");
+  hipLaunchKernelGGL(lhc_encode_long_kernel, dim3((unsigned)std::max<size_t>(1, 2 * max_blocks)), dim3(kEncLongBlock), 0,
+                     stream, len, T, static_cast<uint8_t*>(dst), dst_off, lg);
   return hipGetLastError();
 }
 

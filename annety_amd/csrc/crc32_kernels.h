@@ -242,10 +242,35 @@ hipError_t launch_lhc_compare(const void* stream_base, const uint64_t* off, cons
                               const uint32_t* digest, uint8_t* ok, hipStream_t stream);
 // One pass per frame: CRC, header, payload copy and trailer (crc32_frames.hip lhc_encode_fused_kernel). zero_line:
 // 128 zero bytes (device); img_w8 = the sorted path's image part (kW8ImgBytes, crc32_math.h).
+//
+// Long frames (more than kEncLongMin payload bytes) do not run on one lane group (a 64 MiB frame would be 65k serial
+// rounds): the group claims an entry and the frame's segment descriptors (kSplitSeg, the sorted path's segment
+// format) from this call's counter, writes them and moves on; crc32_var_sorted_kernel then computes the claimed
+// frames' digests, and lhc_encode_long_kernel copies them with the whole grid and writes their headers and trailers.
+// Frames past the caps run on their groups as before. The counters live in the stream slot's extent scratch at
+// kEncCtrOff, one 16-byte set per call parity: {unused, 0 (the sorted kernel's ranges[0]), uint64 {segments (its
+// ranges[1]), frames}}; the long kernel zeroes the next call's set.
+constexpr uint32_t kEncLongMin = 262144;
+constexpr uint32_t kEncLongCap = 4096;         // frames per call
+constexpr uint32_t kEncLongSegCap = 1u << 16;  // segment descriptors per call
+constexpr size_t kEncCtrOff = 8192 - 64;       // after the extent partials, before the bucket cursors
+static_assert((8 + 4 * kExtentMaxParts) * 8 <= kEncCtrOff && kEncCtrOff + 32 <= kCursorOff, "encode counters");
+struct EncLong {
+  unsigned long long* ctr;       // this call's {segments, frames}
+  unsigned long long* ctr_next;  // the next call's (zeroed by lhc_encode_long_kernel)
+  uint32_t* digest;              // [kEncLongCap] preset to ~0, the segments xor into it
+  uint32_t* entry;               // [kEncLongCap] frame index
+  void* desc;                    // [kEncLongSegCap] uint4 segment descriptors
+  uint64_t* seg_dst;             // [kEncLongSegCap] each segment's destination address
+};
+constexpr size_t kEncLongScratchBytes = 8ull * kEncLongCap + 24ull * kEncLongSegCap;  // digest, entry, desc, seg_dst
 hipError_t launch_lhc_encode_fused(const void* src, const uint64_t* src_off, const uint32_t* len, size_t n, int T,
                                    int64_t enc_min, int64_t enc_max, void* dst, const uint64_t* dst_off,
                                    const void* zero_line, const void* img_slice, const void* img_w8,
-                                   size_t max_blocks, hipStream_t stream);
+                                   const EncLong& lg, size_t max_blocks, hipStream_t stream);
+// The claimed long frames: payload copy (16-byte stores over the whole grid, by segment), header and trailer.
+hipError_t launch_lhc_encode_long(const uint32_t* len, int T, void* dst, const uint64_t* dst_off, const EncLong& lg,
+                                  size_t max_blocks, hipStream_t stream);
 int fixed_kernel_block();
 // Records, for annety_crc_last_kernels, that the current entry point enqueued `name` (crc32_capi.cpp).
 void note_kernel(const char* name);

@@ -5,7 +5,9 @@ workload (2M payloads of 16 B - 1 KiB, or 408 B with ENC_FRAMES=chat, or 256K of
   ANNETY_CRC_ENC_PROBE: 0 = the product kernel, 1 = no copy stores, 2 = no CRC, 3 = neither (wrong frames)
 Per setting: microseconds per annety_lhc_encode_batch (HIP events over 200 calls, median of 5 groups), in a child
 process each, alternating twice. ENC_ALIGNED=1 puts each payload at its frame's payload offset in the source, so
-that every store is 16-byte aligned. Usage: python microbench/encode_probe.py [probes...] (default: 0 1 2 3)."""
+that every store is 16-byte aligned. Usage: python microbench/encode_probe.py [probes...] (default: 0 1 2 3).
+ENC_FRAMES=long / longmix: the long-frame path (16 x 64 MiB; 256 x 1 MiB among 200K short); ENC_CALLS = calls per
+group; ENC_LIB = another build of the library (e.g. the one before a change)."""
 import json
 import os
 import subprocess
@@ -29,6 +31,13 @@ def child():
     if kind == "big":  # 256K frames of 4000 B (about the same bytes)
         n = 256 << 10
         lens = np.full(n, 4000, dtype=np.int64)
+    elif kind == "long":  # 16 frames of 64 MiB (the long-frame path, crc32_kernels.h EncLong)
+        n = 16
+        lens = np.full(n, 64 << 20, dtype=np.int64)
+    elif kind == "longmix":  # 256 frames of 1 MiB among 200K of 16 B - 4 KiB
+        lens = np.concatenate([rng.integers(16, 4097, 200000), np.full(256, 1 << 20)])
+        lens = rng.permutation(lens).astype(np.int64)
+        n = lens.size
     else:
         lens = np.full(n, 408, dtype=np.int64) if kind == "chat" else rng.integers(16, 1025, n)
     src_off = np.concatenate([[0], np.cumsum(lens)[:-1]]).astype(np.int64)
@@ -48,23 +57,24 @@ def child():
     s = torch.cuda.current_stream().cuda_stream
 
     def call():
-        st = lib.annety_lhc_encode_batch(src.data_ptr(), d_src_off.data_ptr(), d_len.data_ptr(), n, 4, 1 << 20,
+        st = lib.annety_lhc_encode_batch(src.data_ptr(), d_src_off.data_ptr(), d_len.data_ptr(), n, 4, 1 << 30,
                                          out.data_ptr(), d_foff.data_ptr(), s)
         if st:
             _lib.check(st, "annety_lhc_encode_batch")
 
-    for _ in range(20):
+    calls = int(os.environ.get("ENC_CALLS", "200"))
+    for _ in range(min(20, calls)):
         call()
     torch.cuda.synchronize()
     per = []
     for _ in range(5):
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        for _ in range(200):
+        for _ in range(calls):
             call()
         e1.record()
         torch.cuda.synchronize()
-        per.append(e0.elapsed_time(e1) / 200 * 1e3)
+        per.append(e0.elapsed_time(e1) / calls * 1e3)
     print(json.dumps({"us": sorted(per)[2], "kernels": annety_amd.last_kernels()}))
 
 
@@ -72,7 +82,7 @@ def main():
     if os.environ.get("ENC_PROBE_CHILD"):
         return child()
     settings = sys.argv[1:] or ["0", "1", "2", "3"]
-    lib = os.path.join(ROOT, "microbench", "libannety_crc_ab.so")
+    lib = os.environ.get("ENC_LIB") or os.path.join(ROOT, "microbench", "libannety_crc_ab.so")
     for rep in range(2):
         for pr in settings:
             env = dict(os.environ, ENC_PROBE_CHILD="1", ANNETY_CRC_LIB=lib, ANNETY_CRC_ENC_PROBE=pr)
