@@ -14,7 +14,7 @@ pytestmark = pytest.mark.gpu
 LONG = 262144  # kEncLongMin
 
 
-def _check(gpu, lens, seed, T=4, gap=3, calls=1):
+def _check(gpu, lens, seed, T=4, gap=3, calls=1, max_payload=1 << 30):
     import torch
 
     from annety_amd.codec import LengthHeaderCodec
@@ -25,7 +25,7 @@ def _check(gpu, lens, seed, T=4, gap=3, calls=1):
     offs = np.concatenate([[0], np.cumsum(lens.astype(np.uint64) + gaps)[:-1]]).astype(np.uint64) + 5
     arena = oracle.lcg_bytes(int(offs[-1] + lens[-1]) + 64, seed)
     d_src = torch.from_numpy(arena.copy()).to(gpu)
-    codec = LengthHeaderCodec(T, True, 1 << 30)
+    codec = LengthHeaderCodec(T, True, max_payload)
     kernels = None
     for _ in range(calls):
         r = codec.encode_batch(d_src, offs, lens)
@@ -36,7 +36,7 @@ def _check(gpu, lens, seed, T=4, gap=3, calls=1):
         frames = r.frames.cpu().numpy()
         pos = 0
         for i, (o, L) in enumerate(zip(offs, lens)):
-            rt, want = oracle.lhc_encode(arena[int(o): int(o) + int(L)], T, 1 << 30)
+            rt, want = oracle.lhc_encode(arena[int(o): int(o) + int(L)], T, max_payload)
             got = frames[pos: pos + len(want)].tobytes()
             assert got == want, (i, int(L))
             pos += len(want)
@@ -69,3 +69,8 @@ def test_more_long_frames_than_the_cap(gpu):
 
 def test_two_calls_alternate_counters(gpu):
     _check(gpu, [LONG + 100, 2000, (2 << 20) + 3, 0, 64], 6, calls=3)
+
+
+def test_rejected_long_frames_write_nothing(gpu):
+    # payloads over max_payload get no frame (LengthHeaderCodec::encode :169-176), long or not
+    _check(gpu, [400000, LONG + 5, 290000, 300001, 1000, 300000], 7, max_payload=300000)
