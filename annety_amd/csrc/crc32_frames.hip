@@ -126,9 +126,9 @@ __device__ __forceinline__ bool enc_hand_over(const EncLong& lg, uint64_t A, uin
 // that straddles two segments is whole, loaded from two aligned source chunks and stored once after a byte funnel,
 // and only the payload's first and last chunks are partial (their bytes stored one by one). Thread e < frames
 // stores frame e's header and trailer (as the fused kernel does). Block 0 zeroes the next call's counter.
-constexpr int kEncLongBlock = 512;  // (2 blocks per CU: at 1024 lanes the four chunks in flight spill)
-constexpr int kEncLongIlp = 2;  // segments per block in flight
-constexpr int kEncLongPer = 2;  // chunks per thread and segment in flight (a 16 KiB segment: 1024 chunks)
+constexpr int kEncLongBlock = 256;
+constexpr int kEncLongIlp = 1;  // segments per block in flight
+constexpr int kEncLongPer = 4;  // chunks per thread and segment in flight (a 16 KiB segment: 1024 chunks)
 struct EncSeg {
   uint64_t lo;      // the segment's first owned chunk
   uint64_t nc;      // owned chunks
@@ -155,7 +155,7 @@ __device__ __forceinline__ void enc_chunk_load(EncChunk& ch, const EncSeg& g, ui
   ch.x0 = gload16_nt(l0, 0);
   ch.x1 = gload16_nt(l0, ch.whole && ch.o ? 16u : 0u);
 }
-__device__ __forceinline__ void enc_chunk_store(const EncChunk& ch, const EncSeg& g) {
+__device__ __forceinline__ void enc_chunk_store(const EncChunk& ch) {
   if (ch.whole) {
     const uint32_t w[8] = {ch.x0.x, ch.x0.y, ch.x0.z, ch.x0.w, ch.x1.x, ch.x1.y, ch.x1.z, ch.x1.w};
     const uint32_t qd = ch.o >> 2, sh = ch.o & 3u;
@@ -164,21 +164,22 @@ __device__ __forceinline__ void enc_chunk_store(const EncChunk& ch, const EncSeg
     for (int k = 0; k < 5; k++) y[k] = qd == 0 ? w[k] : (qd == 1 ? w[k + 1] : (qd == 2 ? w[k + 2] : w[k + 3]));
     gstore16_nt(ch.dc, make_uint4(__builtin_amdgcn_alignbyte(y[1], y[0], sh), __builtin_amdgcn_alignbyte(y[2], y[1], sh),
                                   __builtin_amdgcn_alignbyte(y[3], y[2], sh), __builtin_amdgcn_alignbyte(y[4], y[3], sh)));
-  } else if (ch.on) {
-    // the payload's first or last chunk: the <= 2 aligned source chunks holding its payload bytes (both hold one,
-    // so no load leaves the payload's chunks), then the bytes one by one
-    const uint64_t b0 = ch.dc > g.Df ? ch.dc : g.Df, b1 = ch.dc + 16 < g.Ef ? ch.dc + 16 : g.Ef;
-    const uint64_t g0 = (b0 - g.delta) & ~15ull, g1 = (b1 - 1 - g.delta) & ~15ull;
-    const uint4 y0 = gload16(g0), y1 = g1 != g0 ? gload16(g1) : y0;
-    for (uint64_t x = b0; x < b1; x++) {
-      const uint32_t i = (uint32_t)(x - g.delta - g0), q = (i >> 2) & 3u;
-      const uint4 y = i < 16 ? y0 : y1;
-      const uint32_t wd = q == 0 ? y.x : (q == 1 ? y.y : (q == 2 ? y.z : y.w));
-      gstore1(x, wd >> (8 * (i & 3u)));
-    }
   }
 }
-__global__ __launch_bounds__(kEncLongBlock) void lhc_encode_long_kernel(const uint32_t* __restrict__ len, int T,
+// The payload's first or last chunk when it is partial: the <= 2 aligned source chunks holding its payload bytes
+// (both hold one, so no load leaves the payload's chunks), then the bytes one by one.
+__device__ __forceinline__ void enc_chunk_partial(uint64_t dc, const EncSeg& g) {
+  const uint64_t b0 = dc > g.Df ? dc : g.Df, b1 = dc + 16 < g.Ef ? dc + 16 : g.Ef;
+  const uint64_t g0 = (b0 - g.delta) & ~15ull, g1 = (b1 - 1 - g.delta) & ~15ull;
+  const uint4 y0 = gload16(g0), y1 = g1 != g0 ? gload16(g1) : y0;
+  for (uint64_t x = b0; x < b1; x++) {
+    const uint32_t i = (uint32_t)(x - g.delta - g0), q = (i >> 2) & 3u;
+    const uint4 y = i < 16 ? y0 : y1;
+    const uint32_t wd = q == 0 ? y.x : (q == 1 ? y.y : (q == 2 ? y.z : y.w));
+    gstore1(x, wd >> (8 * (i & 3u)));
+  }
+}
+__global__ __launch_bounds__(kEncLongBlock, 5) void lhc_encode_long_kernel(const uint32_t* __restrict__ len, int T,
                                                                      uint8_t* __restrict__ dst,
                                                                      const uint64_t* __restrict__ dst_off,
                                                                      EncLong lg) {
@@ -214,16 +215,21 @@ __global__ __launch_bounds__(kEncLongBlock) void lhc_encode_long_kernel(const ui
 #pragma unroll
     for (int u = 0; u < kEncLongIlp; u++)
 #pragma unroll
-      for (int v = 0; v < kEncLongPer; v++) enc_chunk_store(ch[u][v], g[u]);
-    // the rest of each segment's chunks (the last one of a 16 KiB segment whose destination is not aligned, the
-    // 1 MiB segments')
+      for (int v = 0; v < kEncLongPer; v++) enc_chunk_store(ch[u][v]);
 #pragma unroll
     for (int u = 0; u < kEncLongIlp; u++) {
       if (!on[u]) continue;
+      // the rest of the segment's whole chunks (the 1 MiB segments')
       for (uint64_t q = c + kEncLongPer * kEncLongBlock; q < g[u].nc; q += kEncLongBlock) {
         EncChunk x;
         enc_chunk_load(x, g[u], q, true);
-        enc_chunk_store(x, g[u]);
+        enc_chunk_store(x);
+      }
+      // the payload's partial first chunk (thread 0) and last chunk (thread 1; thread 0 when it is the first too)
+      const bool fs = g[u].Df != 0ull, ls = g[u].Ef != ~0ull;
+      if ((fs && c == 0) || (ls && c == 1 && !(fs && g[u].nc == 1))) {
+        const uint64_t dc = g[u].lo + 16 * (c == 0 ? 0ull : g[u].nc - 1);
+        if (!(dc >= g[u].Df && dc + 16 <= g[u].Ef)) enc_chunk_partial(dc, g[u]);
       }
     }
   }
@@ -530,7 +536,7 @@ hipError_t launch_lhc_encode_fused(const void* src, const uint64_t* src_off, con
 hipError_t launch_lhc_encode_long(const uint32_t* len, int T, void* dst, const uint64_t* dst_off, const EncLong& lg,
                                   size_t max_blocks, hipStream_t stream) {
   note_kernel("lhc_encode_long_kernel");
-  hipLaunchKernelGGL(lhc_encode_long_kernel, dim3((unsigned)std::max<size_t>(1, 2 * max_blocks)), dim3(kEncLongBlock), 0,
+  hipLaunchKernelGGL(lhc_encode_long_kernel, dim3((unsigned)std::max<size_t>(1, 8 * max_blocks)), dim3(kEncLongBlock), 0,
                      stream, len, T, static_cast<uint8_t*>(dst), dst_off, lg);
   return hipGetLastError();
 }
