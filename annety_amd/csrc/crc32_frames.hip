@@ -120,14 +120,13 @@ __device__ __forceinline__ bool enc_hand_over(const EncLong& lg, uint64_t A, uin
 }
 
 // The frames the fused kernel handed over (digests from crc32_var_sorted_kernel): the copy runs over the segment
-// descriptors, a block per segment, two segments per block in flight (their descriptors, destinations and 2 x 512
-// chunks loaded before any store). The destination is cut into aligned 16-byte chunks of the FRAME: a segment owns
+// descriptors, a block per segment (its descriptor and destination loaded an iteration ahead, its first 4 x 256
+// chunks before any store). The destination is cut into aligned 16-byte chunks of the FRAME: a segment owns
 // the chunks that start inside it (the first segment also the one holding the payload's first byte), so a chunk
 // that straddles two segments is whole, loaded from two aligned source chunks and stored once after a byte funnel,
 // and only the payload's first and last chunks are partial (their bytes stored one by one). Thread e < frames
 // stores frame e's header and trailer (as the fused kernel does). Block 0 zeroes the next call's counter.
 constexpr int kEncLongBlock = 256;
-constexpr int kEncLongIlp = 1;  // segments per block in flight
 constexpr int kEncLongPer = 4;  // chunks per thread and segment in flight (a 16 KiB segment: 1024 chunks)
 struct EncSeg {
   uint64_t lo;      // the segment's first owned chunk
@@ -179,7 +178,7 @@ __device__ __forceinline__ void enc_chunk_partial(uint64_t dc, const EncSeg& g) 
     gstore1(x, wd >> (8 * (i & 3u)));
   }
 }
-__global__ __launch_bounds__(kEncLongBlock, 5) void lhc_encode_long_kernel(const uint32_t* __restrict__ len, int T,
+__global__ __launch_bounds__(kEncLongBlock, 4) void lhc_encode_long_kernel(const uint32_t* __restrict__ len, int T,
                                                                      uint8_t* __restrict__ dst,
                                                                      const uint64_t* __restrict__ dst_off,
                                                                      EncLong lg) {
@@ -188,49 +187,43 @@ __global__ __launch_bounds__(kEncLongBlock, 5) void lhc_encode_long_kernel(const
   if (blockIdx.x == 0 && threadIdx.x == 0) *lg.ctr_next = 0ull;
   const uint32_t c = threadIdx.x, nb = gridDim.x;
   const uint4* desc = static_cast<const uint4*>(lg.desc);
-  for (uint32_t k0 = blockIdx.x; k0 < segs; k0 += kEncLongIlp * nb) {
-    EncSeg g[kEncLongIlp];
-    bool on[kEncLongIlp];
+  // the block's next segment's descriptor and destination are loaded one iteration ahead
+  uint4 dn = make_uint4(0, 0, 0, 0);
+  uint64_t Dn = 0;
+  if (blockIdx.x < segs) {
+    dn = desc[blockIdx.x];
+    Dn = lg.seg_dst[blockIdx.x];
+  }
+  for (uint32_t k = blockIdx.x; k < segs; k += nb) {
+    const uint4 d = dn;
+    const uint64_t D0 = Dn;
+    const uint32_t kn = k + nb < segs ? k + nb : k;
+    dn = desc[kn];
+    Dn = lg.seg_dst[kn];
+    EncSeg g;
+    const uint64_t a = ((uint64_t)(d.y & 0xFFFFu) << 32) | d.x, E0 = D0 + d.z;
+    const bool first = (d.w & kSegFirst) != 0, last = (d.y >> 16) == 0;
+    g.lo = first ? D0 & ~15ull : (D0 + 15) & ~15ull;
+    g.nc = ((((E0 - 1) & ~15ull) - g.lo) >> 4) + 1;
+    g.Df = first ? D0 : 0ull;
+    g.Ef = last ? E0 : ~0ull;
+    g.delta = D0 - a;
+    g.safe = a & ~15ull;
+    EncChunk ch[kEncLongPer];
 #pragma unroll
-    for (int u = 0; u < kEncLongIlp; u++) {
-      const uint32_t k = k0 + u * nb;
-      on[u] = k < segs;
-      const uint32_t kk = on[u] ? k : k0;
-      const uint4 d = desc[kk];
-      const uint64_t a = ((uint64_t)(d.y & 0xFFFFu) << 32) | d.x;
-      const uint64_t D0 = lg.seg_dst[kk], E0 = D0 + d.z;
-      const bool first = (d.w & kSegFirst) != 0, last = (d.y >> 16) == 0;
-      g[u].lo = first ? D0 & ~15ull : (D0 + 15) & ~15ull;
-      g[u].nc = ((((E0 - 1) & ~15ull) - g[u].lo) >> 4) + 1;
-      g[u].Df = first ? D0 : 0ull;
-      g[u].Ef = last ? E0 : ~0ull;
-      g[u].delta = D0 - a;
-      g[u].safe = a & ~15ull;
+    for (int v = 0; v < kEncLongPer; v++) enc_chunk_load(ch[v], g, c + v * kEncLongBlock, true);
+#pragma unroll
+    for (int v = 0; v < kEncLongPer; v++) enc_chunk_store(ch[v]);
+    // the rest of the segment's whole chunks (the 1 MiB segments')
+    for (uint64_t q = c + kEncLongPer * kEncLongBlock; q < g.nc; q += kEncLongBlock) {
+      EncChunk x;
+      enc_chunk_load(x, g, q, true);
+      enc_chunk_store(x);
     }
-    EncChunk ch[kEncLongIlp][kEncLongPer];
-#pragma unroll
-    for (int u = 0; u < kEncLongIlp; u++)
-#pragma unroll
-      for (int v = 0; v < kEncLongPer; v++) enc_chunk_load(ch[u][v], g[u], c + v * kEncLongBlock, on[u]);
-#pragma unroll
-    for (int u = 0; u < kEncLongIlp; u++)
-#pragma unroll
-      for (int v = 0; v < kEncLongPer; v++) enc_chunk_store(ch[u][v]);
-#pragma unroll
-    for (int u = 0; u < kEncLongIlp; u++) {
-      if (!on[u]) continue;
-      // the rest of the segment's whole chunks (the 1 MiB segments')
-      for (uint64_t q = c + kEncLongPer * kEncLongBlock; q < g[u].nc; q += kEncLongBlock) {
-        EncChunk x;
-        enc_chunk_load(x, g[u], q, true);
-        enc_chunk_store(x);
-      }
-      // the payload's partial first chunk (thread 0) and last chunk (thread 1; thread 0 when it is the first too)
-      const bool fs = g[u].Df != 0ull, ls = g[u].Ef != ~0ull;
-      if ((fs && c == 0) || (ls && c == 1 && !(fs && g[u].nc == 1))) {
-        const uint64_t dc = g[u].lo + 16 * (c == 0 ? 0ull : g[u].nc - 1);
-        if (!(dc >= g[u].Df && dc + 16 <= g[u].Ef)) enc_chunk_partial(dc, g[u]);
-      }
+    // the payload's partial first chunk (thread 0) and last chunk (thread 1; thread 0 when it is the first too)
+    if ((first && c == 0) || (last && c == 1 && !(first && g.nc == 1))) {
+      const uint64_t dc = g.lo + 16 * (c == 0 ? 0ull : g.nc - 1);
+      if (!(dc >= g.Df && dc + 16 <= g.Ef)) enc_chunk_partial(dc, g);
     }
   }
   const uint64_t gt = blockIdx.x * (uint64_t)kEncLongBlock + threadIdx.x, gs = (uint64_t)gridDim.x * kEncLongBlock;
