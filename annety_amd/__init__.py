@@ -30,6 +30,7 @@ from .crc32c import (  # noqa: F401
     scratch_stats,
     set_frames_pack,
     set_split,
+    set_split_cap,
     set_walk_segment,
     stream_release,
     set_var_path,
@@ -55,6 +56,7 @@ __all__ = [
     "scratch_stats",
     "set_frames_pack",
     "set_split",
+    "set_split_cap",
     "set_walk_segment",
     "stream_release",
     "set_var_path",

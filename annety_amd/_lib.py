@@ -26,6 +26,7 @@ SIGNATURES = [
     ("annety_crc_set_frames_pack", ctypes.c_int, [ctypes.c_int]),
     ("annety_crc_reserve_cus", ctypes.c_int, [ctypes.c_int]),
     ("annety_crc_set_split", ctypes.c_int, [ctypes.c_int, _u64]),
+    ("annety_crc_set_split_cap", ctypes.c_int, [_u32]),
     ("annety_crc_set_walk_segment", ctypes.c_int, [_u64]),
     ("annety_crc_stream_release", ctypes.c_int, [_vp]),
     ("annety_crc_set_var_path", ctypes.c_int, [ctypes.c_int]),

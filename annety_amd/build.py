@@ -42,6 +42,20 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(f) <= t for f in _inputs())
 
 
+def source_digest() -> str:
+    """sha256 (16 hex digits) over the product library's sources and headers (kernels, launchers, C-ABI): what a
+    committed measurement of the kernels (profiles/pmc.py) is stamped with, and what bench.py checks before it
+    reports that measurement as the traffic of the kernels it runs."""
+    import hashlib
+
+    h = hashlib.sha256()
+    for f in sorted(_inputs()):
+        h.update(os.path.basename(f).encode() + b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
+
+
 AB_LIB = os.path.join(ROOT, "microbench", "libannety_crc_ab.so")
 
 

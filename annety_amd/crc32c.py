@@ -102,6 +102,12 @@ def set_split(mode: int = -1, min_segment: int = 0) -> None:
     _lib.check(_lib.get().annety_crc_set_split(int(mode), int(min_segment)), "annety_crc_set_split")
 
 
+def set_split_cap(extra_segments: int = 1 << 18) -> None:
+    """annety_crc_set_split_cap: segment descriptors a sorted-path call may add for its long payloads
+    (default and maximum 2^18; 0 = long payloads run whole), process-wide."""
+    _lib.check(_lib.get().annety_crc_set_split_cap(int(extra_segments)), "annety_crc_set_split_cap")
+
+
 def scratch_stats(device: int = 0) -> dict:
     """annety_crc_scratch_stats: streams holding a scratch slot on `device`, slot hand-overs between
     streams and device-wide synchronisations so far."""

@@ -585,10 +585,11 @@ __device__ __forceinline__ uint32_t bucket_of(uint64_t a, uint32_t len) {
   return (kBucketCount - 1) - (r < kBucketCount - 1 ? r : kBucketCount - 1);
 }
 
-// A payload the sorted path may run as segments (crc32_kernels.h kSplitSeg): digest mode, longer than
-// kSplitMin; its segment size (a uint32 length is < 4096 big segments, within the power tables' reach).
-__device__ __forceinline__ bool split_eligible(const BucketArgs& bk, uint32_t l) {
-  return bk.split_slot && bk.out && l > kSplitMin;
+// A payload the sorted path may run as segments (crc32_kernels.h kSplitSeg): longer than kSplitMin, with an index
+// that fits the segment descriptors; its segment size (a uint32 length is < 4096 big segments, within the power
+// tables' reach).
+__device__ __forceinline__ bool split_eligible(const BucketArgs& bk, size_t i, uint32_t l) {
+  return bk.split_slot && l > kSplitMin && i <= kSegIndexMask;
 }
 __device__ __forceinline__ uint32_t split_seg(uint32_t l) {
   return (uint64_t)l > (uint64_t)kSplitSeg * (kSplitMaxSegs - 1) ? kSplitSegBig : kSplitSeg;
@@ -620,13 +621,18 @@ __global__ __launch_bounds__(kExtentBlock) void crc32_extent_kernel(const uint64
       if (l) {
         const uint64_t a = (uint64_t)(uintptr_t)bk.base + o;
         bool split = false;
-        if (split_eligible(bk, (uint32_t)l)) {  // a long payload: claim its extra descriptors
+        if (split_eligible(bk, i, (uint32_t)l)) {  // a long payload: claim its extra descriptors
           const uint32_t seg = split_seg((uint32_t)l);
           const uint32_t S = (uint32_t)((l + seg - 1) / seg);
-          split = atomicAdd(bk.split_ctr, (unsigned long long)(S - 1)) + (S - 1) <= kSplitSegCap;
+          split = atomicAdd(bk.split_ctr, (unsigned long long)(S - 1)) + (S - 1) <= bk.split_cap;
           bk.split_slot[i] = split ? 1u : 0u;
           if (split) {  // the first segment, then S - 1 of seg bytes with the same alignment, one bucket
-            bk.out[i] = ~0u;  // the segments xor into it
+            if (bk.state) {  // update mode: the first segment starts from the register, the segments xor into 0
+              bk.split_state[i] = bk.state[i];
+              bk.state[i] = 0u;
+            } else {
+              bk.out[i] = ~0u;  // the segments xor into it (the complement of the init's)
+            }
             const uint32_t l0 = (uint32_t)l - (S - 1) * seg;
             atomicAdd(&h[bucket_of(a, l0)], 1u);
             atomicAdd(&h[bucket_of(a + l0, seg)], S - 1);
@@ -688,27 +694,42 @@ __global__ __launch_bounds__(kBucketThreads) void crc32_bucket_place(const uint6
   }
   __syncthreads();
   uint4* desc = static_cast<uint4*>(bk.desc);
-  for (size_t i = blockIdx.x * (size_t)kBucketThreads + t; i < n; i += (size_t)gridDim.x * kBucketThreads) {
-    const uint32_t l = len[i];
-    if (!l) continue;
-    const uint64_t a = (uint64_t)(uintptr_t)bk.base + off[i];
-    if (split_eligible(bk, l) && bk.split_slot[i]) {  // segments: the first (the remainder), then S - 1 of seg bytes
-      const uint32_t seg = split_seg(l), S = (l + seg - 1) / seg, l0 = l - (S - 1) * seg;
-      const uint32_t big = seg == kSplitSegBig ? kSegBig : 0u;
-      const uint32_t p0 = atomicAdd(&basep[bucket_of(a, l0)], 1u);
-      desc[p0] = make_uint4((uint32_t)a, (uint32_t)(a >> 32) | ((S - 1) << 16), l0,
-                            kSegFlag | kSegFirst | big | (uint32_t)i);
-      const uint64_t a1 = a + l0;
-      const uint32_t pk = atomicAdd(&basep[bucket_of(a1, seg)], S - 1);
-      for (uint32_t k = 1; k < S; k++) {
-        const uint64_t ak = a1 + (uint64_t)(k - 1) * seg;
-        desc[pk + k - 1] = make_uint4((uint32_t)ak, (uint32_t)(ak >> 32) | ((S - 1 - k) << 16), seg,
-                                      kSegFlag | big | (uint32_t)i);
-      }
-      continue;
+  // every thread of the block runs the same iterations (the segment writes below take the whole wave)
+  for (size_t i0 = blockIdx.x * (size_t)kBucketThreads; i0 < n; i0 += (size_t)gridDim.x * kBucketThreads) {
+    const size_t i = i0 + t;
+    const uint32_t l = i < n ? len[i] : 0u;
+    const uint64_t a = (uint64_t)(uintptr_t)bk.base + (l ? off[i] : 0ull);
+    const bool split = l && split_eligible(bk, i, l) && bk.split_slot[i];
+    // segments: the first (the remainder), then S - 1 of seg bytes
+    const uint32_t seg = split ? split_seg(l) : 1u, S = split ? (l + seg - 1) / seg : 1u, l0 = l - (S - 1) * seg;
+    uint32_t pk = 0;
+    if (l) {
+      const uint32_t pos = atomicAdd(&basep[bucket_of(a, split ? l0 : l)], 1u);  // LDS atomic: rank in the block's slots
+      desc[pos] = split ? make_uint4((uint32_t)a, (uint32_t)(a >> 32) | ((S - 1) << 16), l0,
+                                     kSegFlag | kSegFirst | (seg == kSplitSegBig ? kSegBig : 0u) | (uint32_t)i)
+                        : make_uint4((uint32_t)a, (uint32_t)(a >> 32), l, (uint32_t)i);
+      if (split) pk = atomicAdd(&basep[bucket_of(a + l0, seg)], S - 1);
     }
-    const uint32_t pos = atomicAdd(&basep[bucket_of(a, l)], 1u);  // LDS atomic: rank inside the block's slots
-    desc[pos] = make_uint4((uint32_t)a, (uint32_t)(a >> 32), l, (uint32_t)i);
+    // the later S - 1 segments of each split payload, written by the whole wave (one thread wrote up to
+    // 16k descriptors of a payload just under 256 MiB in a serial loop)
+    uint64_t pend = __builtin_amdgcn_ballot_w64(split);
+    while (pend) {
+      const int src = __builtin_ffsll((long long)pend) - 1;
+      pend &= pend - 1;
+      const uint32_t sS = (uint32_t)__builtin_amdgcn_readlane((int)S, src);
+      const uint32_t sseg = (uint32_t)__builtin_amdgcn_readlane((int)seg, src);
+      const uint32_t spk = (uint32_t)__builtin_amdgcn_readlane((int)pk, src);
+      const uint32_t si = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)i, src);
+      const uint64_t a1 = a + l0;
+      const uint64_t sa1 = ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(a1 >> 32), src) << 32) |
+                           (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)a1, src);
+      const uint32_t big = sseg == kSplitSegBig ? kSegBig : 0u;
+      for (uint32_t k = 1 + lane; k < sS; k += 64) {
+        const uint64_t ak = sa1 + (uint64_t)(k - 1) * sseg;
+        desc[spk + k - 1] = make_uint4((uint32_t)ak, (uint32_t)(ak >> 32) | ((sS - 1 - k) << 16), sseg,
+                                       kSegFlag | big | si);
+      }
+    }
   }
 }
 

@@ -547,13 +547,20 @@ int scratch_done(DeviceCtx& c, ScratchSlot* slot) {
 // crc32_kernels.h BucketArgs), then one launch per length class with its own lane-group width. Scratch:
 // the stream's slot (scratch_slot): the bucket cursors in the extent area, rows + ranges + descriptors
 // after it.
-// Layout after rows + ranges: descriptors (n, plus kSplitSegCap for long payloads' extra segments), then
-// split_slot (n words; crc32_kernels.h kSplitSeg).
-size_t sorted_desc_count(size_t n) { return n + kSplitSegCap; }
-size_t sorted_scratch_bytes(size_t n) {
-  const size_t rows_words = (size_t)bucket_grid(n) * kBucketCount;
-  return (rows_words + kRangeWords) * sizeof(uint32_t) + 16 * sorted_desc_count(n) + 4 * n;
+// Layout after rows + ranges: descriptors (n, plus split_cap(n) for long payloads' extra segments), then
+// split_slot and split_state (n words each; crc32_kernels.h kSplitSeg).
+// Extra segment descriptors per call (annety_crc_set_split_cap; default and maximum kSplitSegCap).
+std::atomic<uint32_t> g_split_cap{kSplitSegCap};
+// A batch of n payloads never needs more than n * (kSplitMaxSegs - 1) (small batches reserved 4 MiB).
+uint32_t split_cap(size_t n) {
+  return (uint32_t)std::min<uint64_t>(g_split_cap.load(std::memory_order_relaxed), (uint64_t)n * (kSplitMaxSegs - 1));
 }
+size_t sorted_desc_count(size_t n, uint32_t cap) { return n + cap; }
+size_t sorted_scratch_bytes(size_t n, uint32_t cap) {
+  const size_t rows_words = (size_t)bucket_grid(n) * kBucketCount;
+  return (rows_words + kRangeWords) * sizeof(uint32_t) + 16 * sorted_desc_count(n, cap) + 8 * n;
+}
+size_t sorted_scratch_bytes(size_t n) { return sorted_scratch_bytes(n, split_cap(n)); }
 int split_powers(DeviceCtx& c, uint64_t seg, const uint32_t** out);
 
 // The length classes in one launch (the product) or one launch each (A/B builds: ANNETY_CRC_SORTED_FUSED=0).
@@ -567,7 +574,12 @@ bool sorted_fused() {
 int run_var_sorted_in(DeviceCtx& c, ScratchSlot* slot, const void* d_base, size_t n, const uint64_t* d_off,
                       const uint32_t* d_len, uint32_t* d_out, hipStream_t stream, bool update,
                       ExtentHint* record = nullptr, uint64_t seq = 0) {
-  if (n > (size_t)kSegIndexMask) return ANNETY_CRC_EINVAL;  // descriptor indices keep bits 29-31 for segments
+  // descriptor indices keep bit 31 for segments (and payloads past kSegIndexMask run whole)
+  if (n > kSortedMaxPayloads) return ANNETY_CRC_EINVAL;
+  // extra segment descriptors: the cap, within what the slot holds (a setter racing with the sizing cannot overflow it)
+  const size_t fixed = ((size_t)bucket_grid(n) * kBucketCount + kRangeWords) * sizeof(uint32_t) + 24 * n;
+  const uint64_t room = slot->data.bytes > fixed ? (slot->data.bytes - fixed) / 16 : 0;
+  const uint32_t cap = (uint32_t)std::min<uint64_t>(split_cap(n), room);
   uint32_t* cursors = reinterpret_cast<uint32_t*>(static_cast<char*>(slot->data.ptr) + kCursorOff);
   if (!slot->data.cursors_clean) {  // both cursor sets and both split counter sets (contiguous)
     const hipError_t z = hipMemsetAsync(cursors, 0, 2 * kBucketCount * sizeof(uint32_t) + 64, stream);
@@ -591,12 +603,16 @@ int run_var_sorted_in(DeviceCtx& c, ScratchSlot* slot, const void* d_base, size_
   bk.cursor = cursors + set * kBucketCount;
   bk.cursor_next = cursors + (set ^ 1) * kBucketCount;
   bk.out = update ? nullptr : d_out;
+  bk.state = update ? d_out : nullptr;
   unsigned long long* sctr =
       reinterpret_cast<unsigned long long*>(static_cast<char*>(slot->data.ptr) + kSplitCtrOff);
   if (sorted_fused()) {  // (the A/B per-class launches take no segments)
     bk.split_ctr = sctr + 4 * set;
     bk.split_ctr_next = sctr + 4 * (set ^ 1);
-    bk.split_slot = reinterpret_cast<uint32_t*>(static_cast<char*>(bk.desc) + 16 * sorted_desc_count(n));
+    bk.split_slot = reinterpret_cast<uint32_t*>(static_cast<char*>(bk.desc) + 16 * sorted_desc_count(n, cap));
+    bk.split_state = bk.split_slot + n;
+    bk.split_cap = cap;
+    split.state = bk.split_state;
   }
   uint32_t parts = 0;
   hipError_t e = launch_extent(d_off, d_len, n, slot->data.ptr, &parts, &bk, stream);
@@ -1021,6 +1037,12 @@ int annety_crc_set_split(int mode, uint64_t min_segment) {
   return ANNETY_CRC_OK;
 }
 
+int annety_crc_set_split_cap(uint32_t extra_segments) {
+  if (extra_segments > kSplitSegCap) return ANNETY_CRC_EINVAL;
+  g_split_cap.store(extra_segments);
+  return ANNETY_CRC_OK;
+}
+
 int annety_crc_scratch_stats(int device, uint64_t* slots, uint64_t* handoffs, uint64_t* device_syncs) {
   if (device < 0 || device >= kMaxDev) return ANNETY_CRC_ENODEV;
   DeviceCtx& c = g_dev[device];
@@ -1298,6 +1320,7 @@ static int encode_batch(const FrameRules& r, const void* d_src, const uint64_t* 
                         size_t n, void* d_dst, const uint64_t* d_frame_off, void* stream) {
   if (n == 0) return ANNETY_CRC_OK;
   if (!lhc_type_ok(r.T) || !d_src || !d_src_off || !d_len || !d_dst || !d_frame_off) return ANNETY_CRC_EINVAL;
+  if (n > 0xFFFFFFFFull) return ANNETY_CRC_EINVAL;  // the long frames' entries hold 32-bit frame indices
   DeviceCtx* c = nullptr;
   int rc = stream_ctx(static_cast<hipStream_t>(stream), &c);
   if (rc) return rc;

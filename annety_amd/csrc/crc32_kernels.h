@@ -70,18 +70,23 @@ hipError_t launch_var(const VarLaunch& a, hipStream_t stream);
 // .w and m = the segments after it in bits 16-31 of .y (addresses are 48-bit). The group that finishes a segment
 // applies shift_{m seg} to its raw register (the first from the init, the others from 0) from the power table and
 // xors it into out[payload], which the count step preset to ~0, so the digest = ~xor_k shift_{m_k seg}(raw_k)
-// needs no join. Extra descriptors are claimed in the count step up to kSplitSegCap per call; a payload that finds
-// none runs whole.
+// needs no join. Update mode (crc32_update, include/Crc32c.h:71-82) splits the same way: the count step moves the
+// payload's register to SortedSplit::state and presets out[payload] to 0, the first segment starts from that
+// register, and the segments' xor is the new register (no final complement). Extra descriptors are claimed in the
+// count step up to BucketArgs::split_cap (<= kSplitSegCap) per call; a payload that finds none runs whole.
+// Payload indices are 31-bit (bit 31 = kSegFlag); only payloads with index <= kSegIndexMask can split.
 constexpr uint32_t kSplitSeg = 16384;
 constexpr uint32_t kSplitSegBig = 1u << 20;
 constexpr uint32_t kSplitMin = 131072;
 constexpr uint32_t kSplitMaxSegs = 16384;      // the power tables' reach (crc32_capi.cpp kMaxSegs)
-constexpr uint32_t kSplitSegCap = 1u << 18;    // extra descriptors per call
+constexpr uint32_t kSplitSegCap = 1u << 18;    // extra descriptors per call, at most
 constexpr uint32_t kSegFlag = 0x80000000u, kSegFirst = 0x40000000u, kSegBig = 0x20000000u,
                    kSegIndexMask = 0x1FFFFFFFu;
+constexpr uint64_t kSortedMaxPayloads = 0x7FFFFFFFull;  // the sorted list's descriptor indices (bit 31 = kSegFlag)
 struct SortedSplit {
   const uint32_t* powers;      // powers[(m-1)*32 + bit] = shift_{m*kSplitSeg}(1 << bit), m = 1..kSplitMaxSegs-1
   const uint32_t* powers_big;  // the same for kSplitSegBig
+  const uint32_t* state;       // update mode: a split payload's register before it (BucketArgs::split_state)
 };
 // The sorted path in one launch (a.range[0..1] = the sorted list's bounds in a.desc); img_w8 = the w8 image
 // (kW8ImgBytes, crc32_math.h); a.group, a.img_group and a.img_unshift are ignored.
@@ -172,11 +177,13 @@ struct BucketArgs {
   uint32_t* ranges;       // kRangeWords: [0, 1] = {begin, end} of the sorted list in desc, [2..5] empty
   void* desc;             // uint4 {addr lo, addr hi, len, index} per non-empty payload (or segment)
   uint32_t* out;          // zero-length digests; null in update mode
+  uint32_t* state;        // update mode: the registers (null in digest mode)
   // long payloads (launch_var_sorted): null split_slot = no splitting
   unsigned long long* split_ctr;       // this call's counter set (zero on entry)
   unsigned long long* split_ctr_next;  // the other set: zeroed by launch_bucket_place
-  uint32_t* split_slot;                // n words: a long payload's first slot, ~0 when it runs whole
-  uint4* split_rec;                    // kSplitRecCap records
+  uint32_t* split_slot;                // n words: 1 when a long payload runs as segments, else 0
+  uint32_t* split_state;               // update mode, n words: a split payload's register (SortedSplit::state)
+  uint32_t split_cap;                  // extra descriptors this call may claim (<= kSplitSegCap)
 };
 unsigned bucket_grid(size_t n);  // blocks of both launches (= the extent partials: at most kExtentMaxParts)
 

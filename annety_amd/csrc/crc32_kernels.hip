@@ -671,6 +671,13 @@ __device__ __forceinline__ W8Task decode_w8(uint4 d, bool valid) {
   return k;
 }
 // (w8_unshift, w8_join, lane_xor8: crc32_device.h)
+// Update mode: the register a task starts from - the payload's (out[p]); a split payload's first segment takes the
+// register the count step moved aside (out[p] then collects the segments' xor), its later segments start from 0.
+__device__ __forceinline__ uint32_t w8_state(const W8Task& t, const uint32_t* out, const SortedSplit& split) {
+  if (!t.valid) return 0u;
+  if (t.seg) return (t.seg & 1u) ? split.state[t.p] : 0u;
+  return out[t.p];
+}
 
 //   PROBE (A/B builds only, microbench/sorted_probe.py; product = 0): bit 0 = every step takes the unmasked
 //   branch, bit 1 = no fold (the data are xored into the register), bit 2 = loads from config 1's window (wave w,
@@ -753,7 +760,7 @@ __device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restr
   // Pipeline: the load side holds the task whose round rL it loads this step (dL); the compute side (dC, rC) is
   // the load side one step later. Claimed sets [head, tail) wait in the ring (slot = index mod 4).
   W8Task dL = decode_w8(raw(task_of(S0)), task_of(S0) < t_end);
-  if constexpr (UPD) dL.state = dL.valid ? out[dL.p] : 0u;
+  if constexpr (UPD) dL.state = w8_state(dL, out, split);
   uint4 A[8], B[8];
   load(dL, 0, A);
   W8Task dC = dL;
@@ -865,7 +872,7 @@ __device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restr
       if (last && j == G - 1) u = over ? w8_unshift(t, over, lds) : t;
       const bool segl = last && j == G - 1 && cur.seg != 0;
       if (__builtin_amdgcn_ballot_w64(segl) != 0) {
-        // segments: shift_{m seg}(raw) into the payload's digest (preset to ~0). When all 8 groups end segments of
+        // segments: shift_{m seg}(raw) into the payload's digest (preset to ~0; update mode: 0). When all 8 groups end segments of
         // one payload (a long payload's segments are neighbours in the sorted list), one atomic for the wave: one
         // address took every segment's atomic otherwise (16 payloads of 64 MiB: 963 us per call).
         uint32_t x = u;
@@ -905,7 +912,7 @@ __device__ __forceinline__ void var_class_w8(uint4* lds4, const uint8_t* __restr
       head++;
       S0 = ring_set[slot];
       dL = decode_w8(ring[slot * 8 + m], task_of(S0) < t_end);
-      if constexpr (UPD) dL.state = dL.valid ? out[dL.p] : 0u;
+      if constexpr (UPD) dL.state = w8_state(dL, out, split);
       rL = 0;
     }
     maybe_claim(in_new, set_new, pend_new);

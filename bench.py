@@ -42,12 +42,14 @@ METRIC = "CRC-32C GiB/s device-resident (1M×1KiB) @1/2/4/8 MI355X; % HBM roofli
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md (8.0 TB/s)
 # Per-launch HBM bytes from the rocprofv3 PMC passes of this bench's own command (profiles/pmc.sh, FETCH_SIZE x2
 # gfx950 correction + WRITE_SIZE), committed per config; reported as `traffic` with the file as its source
-# (a PMC pass cannot run inside the timed process).
-PMC_FILES_VAR = {"sorted": "profiles/r05/pmc/c3s.json"}  # config 3 on another variable path
-PMC_FILES_FRAMES = {("mixed", "verify"): "profiles/r05/pmc/fmv.json", ("mixed", "encode"): "profiles/r05/pmc/fme.json",
-                    ("chat", "verify"): "profiles/r05/pmc/fcv.json", ("chat", "encode"): "profiles/r05/pmc/fce.json"}
-PMC_FILES = {1: "profiles/r04/config1_pmc.json", 3: "profiles/r05/pmc/c3a.json",
-             2: "profiles/r04/config2_pmc.json", 4: "profiles/r04/config1_pmc.json"}
+# (a PMC pass cannot run inside the timed process). Each summary is stamped with the library's source digest
+# (annety_amd.build.source_digest); a summary whose digest is not the current tree's describes other kernels and is
+# refused (traffic null, `traffic_refused` says why).
+PMC_DIR = "profiles/r06/pmc"
+PMC_FILES_VAR = {"sorted": f"{PMC_DIR}/c3s.json"}  # config 3 on another variable path
+PMC_FILES_FRAMES = {("mixed", "verify"): f"{PMC_DIR}/fmv.json", ("mixed", "encode"): f"{PMC_DIR}/fme.json",
+                    ("chat", "verify"): f"{PMC_DIR}/fcv.json", ("chat", "encode"): f"{PMC_DIR}/fce.json"}
+PMC_FILES = {1: f"{PMC_DIR}/c1.json", 3: f"{PMC_DIR}/c3a.json", 2: f"{PMC_DIR}/c2.json", 4: f"{PMC_DIR}/c1.json"}
 CPU_SAMPLE_BYTES = 1 << 30  # cpu_baseline sample: up to 1 GiB of the workload, far above the host's caches
 # The reference build of oracle/_ref (oracle/Makefile): the reference's Release flags without -march=native.
 REF_FLAGS = "g++ -std=c++11 -O2 -DNDEBUG (CMakeLists.txt:24,48 Release flags; -march=native dropped so the .so runs on any host)"
@@ -415,6 +417,24 @@ def full_check(w: Workload, threads: int) -> dict:
             "seconds": round(time.perf_counter() - t0, 2)}
 
 
+def cgroup_cpu_quota():
+    """CPUs this job's cgroup may use (quota / period), or None when unlimited or unreadable."""
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:  # cgroup v2: "<quota> <period>" or "max <period>"
+            q, per = f.read().split()[:2]
+        return None if q == "max" else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        pass
+    try:  # cgroup v1
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return None if q <= 0 else round(q / per, 2)
+    except (OSError, ValueError):
+        return None
+
+
 def cpu_baseline(h: np.ndarray, offs: np.ndarray, lens: np.ndarray, budget_s: float) -> dict:
     """Reference CPU checksum on this host's cores over a bounded sample of the same workload.
     Uses the compiled reference (oracle/_ref, kind "reference") when it travelled with the snapshot
@@ -454,21 +474,28 @@ def cpu_baseline(h: np.ndarray, offs: np.ndarray, lens: np.ndarray, budget_s: fl
         def run(th):
             oracle.batch_var_mt(h, offs, lens, th)
 
+    import resource
+
     def rate(th, budget):
-        reps, t0 = 0, time.perf_counter()
+        """(GiB/s, passes, CPU-seconds the process got per wall second while running them)"""
+        ru0, reps, t0 = resource.getrusage(resource.RUSAGE_SELF), 0, time.perf_counter()
         while True:
             run(th)
             reps += 1
             dt = time.perf_counter() - t0
             if dt >= budget:
-                return reps * nbytes / dt / 2 ** 30, reps
+                ru1 = resource.getrusage(resource.RUSAGE_SELF)
+                cpu = (ru1.ru_utime - ru0.ru_utime) + (ru1.ru_stime - ru0.ru_stime)
+                return reps * nbytes / dt / 2 ** 30, reps, cpu / dt
 
-    st_rate, st_reps = rate(1, budget_s * 0.3)
-    mt_rate, mt_reps = rate(threads, budget_s * 0.6)
+    st_rate, st_reps, _ = rate(1, budget_s * 0.3)
+    mt_rate, mt_reps, mt_eff = rate(threads, budget_s * 0.6)
     # SURVEY.md §8d(ii): the reference at hardware_concurrency() threads, what annety's one-loop-per-thread
-    # pool (src/EventLoopPool.cc:55-66) would use on this host; the job's scheduler share may cap what these
-    # threads get (affinity_cpus says how many CPUs the process may run on)
-    all_rate, all_reps = rate(host_cpus, budget_s * 0.1) if host_cpus > threads else (mt_rate, mt_reps)
+    # pool (src/EventLoopPool.cc:55-66) would use on this host. The job's CPU quota caps what these threads get:
+    # effective_cpus is the CPU time they actually received per wall second (and cgroup_cpu_quota the quota itself),
+    # which is why os.cpu_count() threads can run no faster than the 16-thread leg (VERDICT r05 item 8).
+    all_rate, all_reps, all_eff = (rate(host_cpus, budget_s * 0.1) if host_cpus > threads
+                                   else (mt_rate, mt_reps, mt_eff))
     try:
         affinity = len(os.sched_getaffinity(0))
     except (AttributeError, OSError):
@@ -477,9 +504,12 @@ def cpu_baseline(h: np.ndarray, offs: np.ndarray, lens: np.ndarray, budget_s: fl
         "value": round(mt_rate, 3),
         "unit": "GiB/s",
         "cores": threads,
+        "effective_cpus": round(mt_eff, 2),
         "host_cpus": host_cpus,
         "all_cores_value": round(all_rate, 3),
         "all_cores": host_cpus,
+        "all_cores_effective_cpus": round(all_eff, 2),
+        "cgroup_cpu_quota": cgroup_cpu_quota(),
         "affinity_cpus": affinity,
         "kind": kind,
         "compile_flags": REF_FLAGS if kind == "reference" else "gcc -O2 (oracle/Makefile, C restatement)",
@@ -491,31 +521,36 @@ def cpu_baseline(h: np.ndarray, offs: np.ndarray, lens: np.ndarray, budget_s: fl
 
 
 def pmc_traffic(w: Workload, var_path: str):
-    """Per-launch HBM bytes of this workload's kernels from the committed rocprofv3 PMC summary
-    (profiles/pmc.sh + pmc.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), summed over the kernels
-    of one step, or None if no summary for this configuration is committed."""
+    """(per-launch HBM bytes, source file, None) of this workload's kernels from the committed rocprofv3 PMC summary
+    (profiles/pmc.sh + pmc.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), summed over the kernels of one step;
+    (None, file, reason) when the summary is missing or was measured on other kernel sources than this tree's."""
+    from annety_amd.build import source_digest
+
     path = PMC_FILES.get(w.config)
     if w.config == 3 and var_path != "arena":
         path = PMC_FILES_VAR.get(var_path)
     if w.config == "frames":
         path = PMC_FILES_FRAMES.get((w.frames_variant, w.op))
     if not path or (w.config in (1, 4) and w.L != 1024):
-        return None
+        return None, None, "no PMC summary for this configuration"
     try:
         with open(os.path.join(ROOT, path)) as f:
             d = json.load(f)
     except (OSError, ValueError):
-        return None
+        return None, path, "summary missing"
+    have, want = d.get("_meta", {}).get("source_digest"), source_digest()
+    if have != want:
+        return None, path, f"stale: measured on library sources {have}, this tree is {want}"
     # the kernels of one step: the library's own list for it (a summary also holds the setup's launches, e.g. the
     # encode that builds the frames stream of a verify step), by name without template arguments
     step = {x.split("<")[0].strip() for x in (w.kernel or "").split("+") if x.strip()}
     tot = sum(v.get("hbm_bytes_per_launch", 0) for k, v in d.items()
-              if ("crc32_" in k or "lhc_" in k) and (not step or k.split("<")[0].strip() in step))
+              if k != "_meta" and ("crc32_" in k or "lhc_" in k) and (not step or k.split("<")[0].strip() in step))
     if not tot:
-        return None
+        return None, path, "no kernel of this step in the summary"
     if w.config == 4:  # the config-1 measurement is per 1M payloads; a config-4 step is n/1M of them
         tot = int(tot * w.n / (1 << 20))
-    return tot, path
+    return tot, path, None
 
 
 def e2e_host_path(w: Workload):
@@ -727,13 +762,13 @@ def main():
     compute_only = None
     if multi:  # the same steps without the gather: value_compute_only, and the roofline's kernel time
         compute_only, kern_ms, _ = timed(args.steps, gather=False)
-    # per-step spread: the same number of steps again, events around groups of steps (up to 20 groups)
-    _, _, per_step = timed(args.steps, gather=False, groups=20)
-    kern_median = float(np.median(per_step))
-    ngroups = len(per_step)
+    # spread: the same K steps again in a pass of its own, a HIP event after every group of >= 10 steps (an event
+    # between two launches costs the stream a few us, so per-step events would time the events: VERDICT r05)
+    spread_groups = max(1, min(20, args.steps // 10))
+    _, _, per_group = timed(args.steps, gather=False, groups=spread_groups)
 
     if rank == 0:
-        traffic = pmc_traffic(w, args.var_path)
+        traffic, traffic_path, traffic_why = pmc_traffic(w, args.var_path)
         cpu = None
         if not (args.no_cpu or multi):
             cs, co, cl = w.host_sample(CPU_SAMPLE_BYTES)
@@ -759,11 +794,6 @@ def main():
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
-            # kernel-stream time per step (HIP events, no gather) over up to 20 consecutive groups of steps, in a
-            # pass of its own right after the timed region
-            "ms_per_step_median": round(kern_median, 4),
-            "ms_per_step_min": round(per_step[0], 4),
-            "ms_per_step_max": round(per_step[-1], 4),
             "higher_is_better": True,
             "scaling": "strong" if args.strong else "weak",
             "vs_baseline": None,
@@ -783,16 +813,21 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic[0] if traffic else None,
-                "traffic_source": (f"{traffic[1]}: rocprofv3 PMC pass (FETCH_SIZE x2 + WRITE_SIZE) of this command, "
-                                   "committed" if traffic else None),
+                "traffic": traffic,
+                "traffic_source": (f"{traffic_path}: rocprofv3 PMC passes (FETCH_SIZE x2 + WRITE_SIZE) of this command, "
+                                   "committed, stamped with this tree's library source digest" if traffic else None),
+                "traffic_refused": None if traffic else {"file": traffic_path, "why": traffic_why},
                 "kernel": steady_kernels,
                 "kernel_source": "annety_crc_last_kernels() after the gate's step (the library's own launch choice)",
+                # HIP events on the launch stream around the timed region's K steps
                 "kernel_ms_avg": round(kern_ms, 4),
-                "kernel_ms_median": round(kern_median, 4),
-                "timing_groups": ngroups,
                 "algorithmic_bytes_per_launch": w.algo_bytes,
             },
+            # a second pass of the same K steps, right after the timed one, with a HIP event after every group of
+            # steps: the kernel-stream time per step within each group (not the timed region's)
+            "step_spread": {"groups": len(per_group), "steps_per_group": args.steps // len(per_group),
+                            "min_ms": round(per_group[0], 4), "median_ms": round(float(np.median(per_group)), 4),
+                            "max_ms": round(per_group[-1], 4)},
             "cpu_baseline": cpu,
             "checked_vs_oracle": checked,
         }

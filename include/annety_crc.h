@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define ANNETY_CRC_ABI_VERSION 5
+#define ANNETY_CRC_ABI_VERSION 6
 
 enum {
   ANNETY_CRC_OK = 0,
@@ -80,6 +80,11 @@ int annety_crc_reserve_cus(int n);
  * payload spans two segments; min_segment = smallest segment in bytes (power of two >= 4096), 0 = default
  * 64 KiB. Digests do not depend on it. */
 int annety_crc_set_split(int mode, uint64_t min_segment);
+/* Variable batches on the length-sorted path run each payload of more than 128 KiB as 16 KiB segments (1 MiB
+ * segments past 256 MiB), digests and update registers alike. extra_segments bounds the segment descriptors one
+ * call may add (default and maximum 262144 = 2^18, 4 MiB of per-stream scratch; 0 = never split); payloads that
+ * find no room run whole. Process-wide; results do not depend on it. ANNETY_CRC_EINVAL above the maximum. */
+int annety_crc_set_split_cap(uint32_t extra_segments);
 /* Host frame walks (annety_lhc_parse, annety_*_verify_host*): a buffer of at least two segments of
  * `bytes` (0 = default 64 MiB, at least 4096) is walked in segments side by side, each later segment from
  * a speculative entry that the in-order join confirms or redoes (crc32_capi.cpp FrameWalks). Results do
@@ -135,7 +140,8 @@ int annety_crc32_batch_fixed(const void* d_base, size_t n, size_t len, size_t st
  * and the device check: the span is checked on the host to lie inside one device allocation (so the line
  * pass reads only mapped memory), and the stitch folds any payload outside the span from its own bytes. In
  * every call each digest depends only on its payload's bytes: a changed layout costs time, never a wrong
- * digest or a read of unmapped memory. ANNETY_CRC_VAR_AUTO=0: sorted path only. */
+ * digest or a read of unmapped memory. ANNETY_CRC_VAR_AUTO=0: sorted path only.
+ * n must be below 2^31 (ANNETY_CRC_EINVAL otherwise): the sorted list keeps bit 31 of an index for segments. */
 int annety_crc32_batch_var(const void* d_base, const uint64_t* d_off, const uint32_t* d_len, size_t n,
                            uint32_t* d_out, void* stream);
 /* Raw-register update (crc32_update semantics) for a fixed-length batch: d_state[i] is the register
@@ -145,7 +151,8 @@ int annety_crc32_update_batch_fixed(uint32_t* d_state, const void* d_base, size_
 /* Streaming update: one fragment per stream, fragment i = [d_base + d_off[i],
  * + d_len[i]) advances stream i's register d_state[i] in place (crc32_update, include/Crc32c.h:71-82).
  * A fragment of length 0 leaves its register unchanged. Seed with 0xFFFFFFFF and xor the final register
- * with 0xFFFFFFFF to get crc32_long of the whole stream. */
+ * with 0xFFFFFFFF to get crc32_long of the whole stream. Path choice, the split of long fragments and the
+ * bound on n as annety_crc32_batch_var. */
 int annety_crc32_update_batch_var(uint32_t* d_state, const void* d_base, const uint64_t* d_off, const uint32_t* d_len,
                                   size_t n, void* stream);
 

@@ -1,6 +1,9 @@
 """Summarise profiles/pmc.sh passes: per kernel, the median per launch of every counter, and HBM bytes
 = 2 x FETCH_SIZE (KiB) x 1024 + WRITE_SIZE (KiB) x 1024 (gfx950: FETCH_SIZE counts half of a wide
-streaming read, MI355X_MICROARCH.md §HBM).  Usage: python profiles/pmc.py gpurun_out/pmc_<tag> [out.json]"""
+streaming read, MI355X_MICROARCH.md §HBM).  Usage: python profiles/pmc.py gpurun_out/pmc_<tag> [out.json]
+The summary carries "_meta": the library's source digest (annety_amd.build.source_digest) of the tree the passes
+ran from, and the bench arguments; bench.py reports the file as `traffic` only while that digest is the current
+one."""
 import collections
 import csv
 import glob
@@ -8,6 +11,9 @@ import json
 import os
 import statistics
 import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from annety_amd.build import source_digest  # noqa: E402
 
 src = sys.argv[1]
 vals = collections.defaultdict(lambda: collections.defaultdict(list))
@@ -28,6 +34,11 @@ for k, cs in vals.items():
         t = m["TCC_HIT_sum"] + m["TCC_MISS_sum"]
         m["l2_hit_rate"] = m["TCC_HIT_sum"] / t if t else None
     res[k] = m
+args = ""
+if os.path.exists(os.path.join(src, "args.txt")):
+    args = open(os.path.join(src, "args.txt")).read().strip()
+res["_meta"] = {"source_digest": source_digest(), "bench_args": args,
+                "counters": "FETCH_SIZE, WRITE_SIZE, TCC_HIT_sum + TCC_MISS_sum: one rocprofv3 --pmc pass each"}
 print(json.dumps(res, indent=1))
 if len(sys.argv) > 2:
     with open(sys.argv[2], "w") as f:

@@ -8,6 +8,7 @@ TAG=$1; shift
 R=$GRAFT_REPO_ROOT
 OUT=$R/gpurun_out/pmc_$TAG
 mkdir -p $OUT
+echo "$@" > $OUT/args.txt
 cd /tmp && export TMPDIR=/tmp
 i=0
 for P in "FETCH_SIZE" "WRITE_SIZE" "TCC_HIT_sum TCC_MISS_sum"; do

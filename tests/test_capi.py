@@ -208,6 +208,9 @@ def test_boundary_error_paths_without_device():
     assert lib.annety_crc_set_split(1, 5000) == -1  # segment not a power of two
     assert lib.annety_crc_set_split(1, 1024) == -1  # segment below 4 KiB
     assert lib.annety_crc_set_split(-1, 0) == 0
+    assert lib.annety_crc_set_split_cap((1 << 18) + 1) == -1  # above kSplitSegCap
+    assert lib.annety_crc_set_split_cap(0) == 0
+    assert lib.annety_crc_set_split_cap(1 << 18) == 0
     v = [ctypes.c_uint64(7) for _ in range(3)]
     assert lib.annety_crc_scratch_stats(-1, *[ctypes.byref(x) for x in v]) == -4
     assert lib.annety_crc_scratch_stats(0, *[ctypes.byref(x) for x in v]) == 0
