@@ -32,7 +32,7 @@ SIGNATURES = [
     ("annety_crc_set_var_path", ctypes.c_int, [ctypes.c_int]),
     ("annety_crc_get_var_path", ctypes.c_int, []),
     ("annety_crc_var_path_stats", ctypes.c_int,
-     [ctypes.c_int, ctypes.POINTER(_u64), ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
+     [ctypes.c_int, ctypes.POINTER(_u64), ctypes.POINTER(_u64), ctypes.POINTER(_u64), ctypes.POINTER(_u64)]),
     ("annety_crc_scratch_stats", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_u64), ctypes.POINTER(_u64),
                                                 ctypes.POINTER(_u64)]),
     ("annety_crc32_long", _u32, [_vp, _c_size]),

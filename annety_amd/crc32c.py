@@ -133,14 +133,15 @@ def set_var_path(path: str) -> str:
 
 
 def var_path_stats(device: int = 0) -> dict:
-    """annety_crc_var_path_stats: how many automatic variable-batch calls took the arena / sorted path, and
-    how many of the arena calls ran without recording their extent ("arena_unrecorded")."""
+    """annety_crc_var_path_stats: how many automatic variable-batch calls the host sent to the arena / sorted path
+    from recorded extents, how many of those arena calls ran without recording their extent ("arena_unrecorded"),
+    and how many calls the device chose for ("device")."""
     import ctypes
 
-    a, b, u = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
-    _lib.check(_lib.get().annety_crc_var_path_stats(int(device), ctypes.byref(a), ctypes.byref(b), ctypes.byref(u)),
-               "annety_crc_var_path_stats")
-    return {"arena": a.value, "sorted": b.value, "arena_unrecorded": u.value}
+    a, b, u, d = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    _lib.check(_lib.get().annety_crc_var_path_stats(int(device), ctypes.byref(a), ctypes.byref(b), ctypes.byref(u),
+                                                    ctypes.byref(d)), "annety_crc_var_path_stats")
+    return {"arena": a.value, "sorted": b.value, "arena_unrecorded": u.value, "device": d.value}
 
 
 def stream_release(stream) -> None:

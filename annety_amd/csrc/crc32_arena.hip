@@ -110,7 +110,27 @@ struct StitchGeo {
   bool check_any_order;
   ExtentHint* record;
   uint64_t record_seq;
+  AutoChoice choice;  // ArenaLaunch::choice: W0 = the scratch, the geometry from the device's span
 };
+
+// The stitch's geometry for the span the device chose (AutoChoice; the host's stitch_geo below).
+__device__ __forceinline__ void stitch_geo_chosen(StitchGeo& s, const ArenaSpan& sp, const ArenaGeom& geo) {
+  uint32_t* scratch = const_cast<uint32_t*>(s.W0);
+  s.byte_lo = sp.byte_lo;
+  s.byte_hi = sp.byte_hi;
+  s.line_lo = sp.line_lo;
+  s.line_hi = sp.line_hi;
+  s.sb0 = sp.sb0;
+  s.fs0 = sp.fs0;
+  s.fs1 = sp.fs1;
+  s.S = scratch;  // (W, L and Lmagic: the host's, from choice.blocks)
+  s.SB = scratch + geo.sb_off;
+  s.S_edge = scratch + geo.edge_off;
+  s.SB_edge = scratch + geo.edge_off + 128;
+  s.sb_word = (uint32_t)geo.sb_off;
+  s.edge_word = (uint32_t)geo.edge_off;
+  s.check = nullptr;
+}
 
 // One payload's loads and the plan that consumes them. Steps 0..3 = head block, first partial
 // superblock's blocks, last partial superblock's blocks, tail block; mid = whole superblocks between.
@@ -430,6 +450,16 @@ __global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchGeo g0, c
                                                                  const uint4* __restrict__ img_stitch) {
   __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsStitchImageBytes / 16];
   StitchGeo g = g0;
+  if (g.choice.ws) {  // the device's choice: the arena's span (or return: the sorted path runs this call)
+    ArenaSpan sp;
+    if (!choose_arena(g.choice, sp)) return;
+    stitch_geo_chosen(g, sp, arena_geom_of(sp.fs1 - sp.fs0, g.choice.blocks));
+    if (blockIdx.x == 0 && threadIdx.x == 0 && g.record) {  // the next calls' record (crc32_kernels.h)
+      uint64_t lo, hi, sum, bad;
+      extent_of(g.choice.ws, g.choice.parts, lo, hi, sum, bad);
+      publish_extent(g.record, lo, hi, sum, bad, g.record_seq);
+    }
+  }
   // automatic path: this call's extent, reduced by every wave from the partials; on a mismatch with the
   // declared arena the line pass did nothing, and every payload is folded directly
   if (g.check) {
@@ -509,12 +539,20 @@ __global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchGeo g0, c
 }
 
 // First launch: the line pass.
+// `base` = the first full superblock (fs0 * 8192); with a device choice (ar.choice.ws) the batch's base, from which
+// the pass moves to the chosen span's first full superblock (or returns: the sorted path runs this call).
 template <int PROBE = 0, bool NT = true>
 __global__ __launch_bounds__(kBlock) void crc32_arena_lines_kernel(const uint8_t* __restrict__ base, LineOut ar,
                                                                    const uint4* __restrict__ img_slice,
                                                                    const uint4* __restrict__ img_group8,
                                                                    const uint4* __restrict__ img_sb) {
   __shared__ __attribute__((aligned(16))) uint4 lds4[(NT ? kLdsArenaNtImageBytes : kLdsArenaImageBytes) / 16];
+  if (ar.choice.ws) {
+    ArenaSpan sp;
+    if (!choose_arena(ar.choice, sp)) return;  // uniform over the grid
+    line_out_chosen(ar, sp, arena_geom_of(sp.fs1 - sp.fs0, gridDim.x));
+    base += (int64_t)(sp.fs0 * 8192 - (uint64_t)(uintptr_t)base);
+  }
   arena_line_pass<PROBE, NT>(base, ar, blockIdx.x, gridDim.x, lds4, img_slice, img_group8, img_sb);
 }
 
@@ -560,7 +598,7 @@ __device__ __forceinline__ void block_reduce4(uint64_t lo, uint64_t hi, uint64_t
     red[3][w] = bad;
   }
   __syncthreads();
-  if (threadIdx.x == 0) {
+  if (threadIdx.x == 0 && out) {
     for (int k = 1; k < kExtentBlock / 64; k++) {
       lo = min(lo, red[0][k]);
       hi = max(hi, red[1][k]);
@@ -602,6 +640,10 @@ __global__ __launch_bounds__(kExtentBlock) void crc32_extent_kernel(const uint64
                                                                     uint64_t* ws, BucketArgs bk) {
   __shared__ uint32_t h[COUNT ? kBucketCount : 1];
   if constexpr (COUNT) {
+    if (bk.choice.ws) {  // the device's choice (AutoChoice): nothing to do when it is the arena
+      ArenaSpan sp;
+      if (choose_arena(bk.choice, sp)) return;
+    }
     for (uint32_t i = threadIdx.x; i < kBucketCount; i += kExtentBlock) h[i] = 0;
     __syncthreads();
   }
@@ -644,7 +686,8 @@ __global__ __launch_bounds__(kExtentBlock) void crc32_extent_kernel(const uint64
       }
     }
   }
-  block_reduce4(lo, hi, sum, bad, ws + 8 + 4 * (size_t)blockIdx.x);  // (its barrier also orders h)
+  // (its barrier also orders h; with a device choice the partials are the extent kernel's, already in ws)
+  block_reduce4(lo, hi, sum, bad, COUNT && bk.choice.ws ? nullptr : ws + 8 + 4 * (size_t)blockIdx.x);
   if constexpr (COUNT) {
     __syncthreads();
     uint32_t* row = bk.rows + (size_t)blockIdx.x * kBucketCount;
@@ -664,6 +707,16 @@ __global__ __launch_bounds__(kBucketThreads) void crc32_bucket_place(const uint6
   __shared__ uint32_t basep[kBucketCount];
   __shared__ uint32_t wtot[kBucketThreads / 64];
   const uint32_t t = threadIdx.x, lane = t & 63, w = t >> 6;
+  if (bk.choice.ws) {  // the device's choice (AutoChoice): when it is the arena, only the next call's sets are zeroed
+    ArenaSpan sp;
+    if (choose_arena(bk.choice, sp)) {
+      if (blockIdx.x == 0) {
+        bk.cursor_next[t] = 0u;
+        if (bk.split_ctr_next && t == 0) *bk.split_ctr_next = 0ull;
+      }
+      return;
+    }
+  }
   // bucket totals (step 1's atomics, finished at the kernel boundary) -> exclusive bucket bases
   const uint32_t tot = __hip_atomic_load(bk.cursor + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   const uint32_t mine = bk.rows[(size_t)blockIdx.x * kBucketCount + t];  // valid where this block has payloads
@@ -785,6 +838,7 @@ LineOut line_out(const ArenaLaunch& a, const ArenaGeom& geo) {
   ar.check_lo = a.check_lo;
   ar.check_any_order = a.check_any_order;
   ar.check_hi = a.check_hi;
+  ar.choice = a.choice;  // (with a device choice the kernel derives the geometry from S = the scratch)
   return ar;
 }
 
@@ -825,12 +879,19 @@ StitchGeo stitch_geo(const ArenaLaunch& a, const ArenaGeom& geo) {
   s.check_hi = a.check_hi;
   s.record = a.record;
   s.record_seq = a.record_seq;
+  s.choice = a.choice;  // (with a device choice the kernel derives the geometry from W0 = the scratch)
   return s;
+}
+
+// The geometry the host launches with: the arena's, or with a device choice (ArenaLaunch::choice) the line pass on
+// choice.blocks workgroups over a span the kernels find themselves.
+ArenaGeom launch_geom(const ArenaLaunch& a) {
+  return a.choice.ws ? arena_geom_of(0, a.choice.blocks) : arena_geom(a);
 }
 
 template <int PROBE, int PIPE = 0, int BLK = kStitchBlock, bool MID = false>
 hipError_t launch_stitch_p(const ArenaLaunch& a, hipStream_t stream) {
-  const StitchGeo s = stitch_geo(a, arena_geom(a));
+  const StitchGeo s = stitch_geo(a, launch_geom(a));
   const size_t blocks = stitch_blocks(a, BLK);
   const uint4* img_slice = static_cast<const uint4*>(a.img_slice);
   const uint4* img_stitch = static_cast<const uint4*>(a.img_stitch);
@@ -853,10 +914,13 @@ hipError_t launch_stitch_p(const ArenaLaunch& a, hipStream_t stream) {
 template <int PROBE, bool NT = true>
 hipError_t launch_arena_lines_p(const ArenaLaunch& a, hipStream_t stream) {
   static_assert(kBlock / 8 == 64 && kSTasks % 4 == 0, "arena_geom / arena_s_word assume 64 groups per block, bursts of 4k tasks");
-  const ArenaGeom geo = arena_geom(a);
+  const ArenaGeom geo = launch_geom(a);
+  // the first full superblock, or with a device choice the batch's base (the kernel moves to the span it finds)
+  const uint8_t* base = a.choice.ws ? static_cast<const uint8_t*>(a.base)
+                                    : reinterpret_cast<const uint8_t*>((uintptr_t)(a.fs0 * 8192));
   note_kernel("crc32_arena_lines_kernel");
-  hipLaunchKernelGGL((crc32_arena_lines_kernel<PROBE, NT>), dim3((unsigned)geo.blocks), dim3(kBlock), 0, stream,
-                     reinterpret_cast<const uint8_t*>((uintptr_t)(a.fs0 * 8192)), line_out(a, geo), static_cast<const uint4*>(a.img_slice), static_cast<const uint4*>(a.img_group8),
+  hipLaunchKernelGGL((crc32_arena_lines_kernel<PROBE, NT>), dim3((unsigned)geo.blocks), dim3(kBlock), 0, stream, base,
+                     line_out(a, geo), static_cast<const uint4*>(a.img_slice), static_cast<const uint4*>(a.img_group8),
                      static_cast<const uint4*>(a.img_sb));
   return hipGetLastError();
 }
@@ -874,7 +938,7 @@ hipError_t launch_arena_lines(const ArenaLaunch& a, hipStream_t stream) {
 }
 
 hipError_t launch_arena(const ArenaLaunch& a, hipStream_t stream) {
-  if (a.nsb) {
+  if (a.nsb || a.choice.ws) {
     const hipError_t e = launch_arena_lines(a, stream);
     if (e != hipSuccess) return e;
   }

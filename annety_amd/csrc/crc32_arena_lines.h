@@ -19,29 +19,27 @@ struct LineOut {
   uint32_t check_parts;
   uint64_t check_lo, check_hi;
   bool check_any_order;
+  AutoChoice choice;  // ArenaLaunch::choice: S = the scratch, the rest from the device's span (line_out_chosen)
 };
 
-// This call's extent from the launch_extent partials (ws + 8 + 4b: {lo, hi, sum, bad} of block b), reduced
-// by the calling wave; every wave computes the same values.
-__device__ __forceinline__ void extent_of(const uint64_t* ws, uint32_t parts, uint64_t& lo, uint64_t& hi,
-                                          uint64_t& sum, uint64_t& bad) {
-  lo = ~0ull;
-  hi = sum = bad = 0;
-  for (uint32_t b = threadIdx.x & 63; b < parts; b += 64) {
-    const uint64_t* q = ws + 8 + 4 * (size_t)b;
-    lo = min(lo, q[0]);
-    hi = max(hi, q[1]);
-    sum += q[2];
-    bad |= q[3];
-  }
-#pragma unroll
-  for (int d = 32; d >= 1; d >>= 1) {
-    lo = min(lo, (uint64_t)__shfl_xor((unsigned long long)lo, d));
-    hi = max(hi, (uint64_t)__shfl_xor((unsigned long long)hi, d));
-    sum += (uint64_t)__shfl_xor((unsigned long long)sum, d);
-    bad |= (uint64_t)__shfl_xor((unsigned long long)bad, d);
-  }
+// The line pass's geometry for the span the device chose (AutoChoice; the host's line_out in crc32_arena.hip).
+__device__ __forceinline__ void line_out_chosen(LineOut& ar, const ArenaSpan& sp, const ArenaGeom& geo) {
+  ar.SB = ar.S + geo.sb_off;
+  ar.S_edge = ar.S + geo.edge_off;
+  ar.SB_edge = ar.S_edge + 128;
+  ar.W = geo.W;
+  ar.byte_lo = sp.byte_lo;
+  ar.byte_hi = sp.byte_hi;
+  ar.line_lo = sp.line_lo;
+  ar.line_hi = sp.line_hi;
+  ar.sb0 = sp.sb0;
+  ar.nsb = sp.nsb;
+  ar.fs0 = sp.fs0;
+  ar.fs1 = sp.fs1;
+  ar.check = nullptr;
 }
+
+// (extent_of, choose_arena: crc32_device.h)
 // ArenaLaunch::check: this call's extent equals the declared one and the batch is safe (sorted with small gaps,
 // or any order when the host found the declared span inside one allocation: any_order).
 __device__ __forceinline__ bool extent_matches(const uint64_t* check, uint32_t parts, uint64_t lo, uint64_t hi,

@@ -284,6 +284,7 @@ struct Scratch {
       return base == o.base && off == o.off && len == o.len && n == o.n && update == o.update;
     }
   } key{};
+  uint64_t arena_want = 0;                // scratch bytes the densest span recorded in this slot needs (any key)
   uint64_t key_since = 0;                 // first call (seq) with the current key
   uint64_t since_extent = 0;              // arena calls since the last one that recorded its extent
   uint64_t seen_seq = 0, prev_seq = 0;    // the two latest completed hints read for this key
@@ -348,6 +349,7 @@ struct DeviceCtx {
   std::atomic<uint64_t> shutdown_syncs{0};
   std::atomic<uint64_t> auto_arena{0}, auto_sorted{0};  // run_var_auto's choices
   std::atomic<uint64_t> auto_unchecked{0};              // arena calls without the extent kernel
+  std::atomic<uint64_t> auto_device{0};                 // calls whose path the device chose (AutoChoice)
 };
 
 constexpr int kMaxDev = 64;
@@ -573,7 +575,7 @@ bool sorted_fused() {
 // (automatic path): the extent record the bucket pass publishes, numbered `seq`.
 int run_var_sorted_in(DeviceCtx& c, ScratchSlot* slot, const void* d_base, size_t n, const uint64_t* d_off,
                       const uint32_t* d_len, uint32_t* d_out, hipStream_t stream, bool update,
-                      ExtentHint* record = nullptr, uint64_t seq = 0) {
+                      ExtentHint* record = nullptr, uint64_t seq = 0, const AutoChoice* choice = nullptr) {
   // descriptor indices keep bit 31 for segments (and payloads past kSegIndexMask run whole)
   if (n > kSortedMaxPayloads) return ANNETY_CRC_EINVAL;
   // extra segment descriptors: the cap, within what the slot holds (a setter racing with the sizing cannot overflow it)
@@ -604,6 +606,7 @@ int run_var_sorted_in(DeviceCtx& c, ScratchSlot* slot, const void* d_base, size_
   bk.cursor_next = cursors + (set ^ 1) * kBucketCount;
   bk.out = update ? nullptr : d_out;
   bk.state = update ? d_out : nullptr;
+  if (choice) bk.choice = *choice;
   unsigned long long* sctr =
       reinterpret_cast<unsigned long long*>(static_cast<char*>(slot->data.ptr) + kSplitCtrOff);
   if (sorted_fused()) {  // (the A/B per-class launches take no segments)
@@ -634,10 +637,12 @@ int run_var_sorted_in(DeviceCtx& c, ScratchSlot* slot, const void* d_base, size_
     a.img_unshift = c.d_unshift;
     a.out = d_out;
     a.max_blocks = grid_cus(c);
+    if (choice) a.choice = *choice;
     const hipError_t e = launch_var_sorted(a, c.d_w8, split, stream);
     return e == hipSuccess ? ANNETY_CRC_OK : hip_fail(e);
   }
-  // (A/B builds) the per-task var kernel over the sorted list, 32 lanes per payload
+  // (A/B builds) the per-task var kernel over the sorted list, 32 lanes per payload (no device choice)
+  if (choice) return ANNETY_CRC_EINVAL;
   rc = run_var(c, d_base, n, 0, 0, 32, bk.desc, bk.ranges, d_out, stream, update);
   return rc;
 }
@@ -666,15 +671,15 @@ void arena_fill_range(const DeviceCtx& c, const void* d_base, uint64_t byte_lo, 
   a.zero_line = c.d_zero;
   a.max_blocks = grid_cus(c);
   if (byte_hi <= byte_lo) return;
-  a.byte_lo = byte_lo;
-  a.byte_hi = byte_hi;
-  a.line_lo = a.byte_lo >> 7;
-  a.line_hi = (a.byte_hi - 1) >> 7;
-  a.sb0 = a.line_lo >> 6;
-  a.nsb = (a.line_hi >> 6) - a.sb0 + 1;
-  a.fs0 = (a.byte_lo + 8191) >> 13;  // superblocks wholly inside the arena
-  a.fs1 = a.byte_hi >> 13;
-  if (a.fs1 < a.fs0) a.fs1 = a.fs0;
+  const ArenaSpan sp = arena_span(byte_lo, byte_hi);
+  a.byte_lo = sp.byte_lo;
+  a.byte_hi = sp.byte_hi;
+  a.line_lo = sp.line_lo;
+  a.line_hi = sp.line_hi;
+  a.sb0 = sp.sb0;
+  a.nsb = sp.nsb;
+  a.fs0 = sp.fs0;
+  a.fs1 = sp.fs1;
 }
 
 void arena_fill(const DeviceCtx& c, const void* d_base, size_t arena_bytes, ArenaLaunch& a) {
@@ -763,6 +768,28 @@ bool poll_hint(ScratchSlot* slot) {
   return true;
 }
 
+// Whether a completed record allows the arena path: a dense span (payload bytes >= 2/3 of it, under 32 GiB) that is
+// safe to read - sorted starts with gaps < 4 KiB, or (host check) inside one device allocation.
+bool record_allows_arena(const ExtentHint& h, uint64_t b) {
+  if (!(h.hi > h.lo && h.sum * 3 >= (h.hi - h.lo) * 2 && h.hi - h.lo < (32ull << 30))) return false;
+  return !h.bad || range_mapped(b + h.lo, b + h.hi);
+}
+
+// The slot's latest completed record, whatever pointers it was for (false if none or torn).
+bool latest_hint(const ScratchSlot* slot, ExtentHint* out) {
+  const ExtentHint* p = slot->data.hint;
+  ExtentHint h{};
+  h.lo = __atomic_load_n(&p->lo, __ATOMIC_RELAXED);
+  h.hi = __atomic_load_n(&p->hi, __ATOMIC_RELAXED);
+  h.sum = __atomic_load_n(&p->sum, __ATOMIC_RELAXED);
+  h.bad = __atomic_load_n(&p->bad, __ATOMIC_RELAXED);
+  h.seq = __atomic_load_n(&p->seq, __ATOMIC_RELAXED);
+  h.chk = __atomic_load_n(&p->chk, __ATOMIC_RELAXED);
+  if (h.seq == 0 || (h.lo ^ h.hi ^ h.sum ^ h.bad ^ h.seq ^ kExtentCheck) != h.chk) return false;
+  *out = h;
+  return true;
+}
+
 int run_var_auto(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_off, const uint32_t* d_len,
                  uint32_t* d_out, hipStream_t stream, bool update) {
   if (n < kAutoMinPayloads) return run_var_sorted(c, d_base, n, d_off, d_len, d_out, stream, update);
@@ -782,16 +809,25 @@ int run_var_auto(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_o
     slot->data.since_extent = 0;
   }
   poll_hint(slot);
+  {  // the arena scratch that the densest span recorded here needs (whatever pointers it was for), so that a device
+     // choice on fresh pointers of a similar batch finds room for it (the span's alignment can add a superblock at
+     // each end)
+    ExtentHint lh{};
+    if (latest_hint(slot, &lh) && lh.hi > lh.lo && lh.sum * 3 >= (lh.hi - lh.lo) * 2 && lh.hi - lh.lo < (32ull << 30))
+      slot->data.arena_want = std::max<uint64_t>(
+          slot->data.arena_want, arena_geom_of(((lh.hi - lh.lo) >> 13) + 2, grid_cus(c)).words * sizeof(uint32_t));
+  }
   const ExtentHint& h = slot->data.seen;
   const uint64_t b = (uint64_t)(uintptr_t)d_base;
-  bool arena = slot->data.seen_seq >= slot->data.key_since && slot->data.prev_seq >= slot->data.key_since &&
-               h.hi > h.lo && h.lo == slot->data.prev.lo && h.hi == slot->data.prev.hi &&
-               h.sum * 3 >= (h.hi - h.lo) * 2 && h.hi - h.lo < (32ull << 30);
+  const bool have1 = slot->data.seen_seq >= slot->data.key_since;                // a completed record for these pointers
+  const bool have2 = have1 && slot->data.prev_seq >= slot->data.key_since;       // and the one before it
+  const bool allow_h = have1 && record_allows_arena(h, b);
+  bool arena = have2 && allow_h && h.lo == slot->data.prev.lo && h.hi == slot->data.prev.hi &&
+               slot->data.prev.sum * 3 >= (h.hi - h.lo) * 2;
   // Safe: sorted starts with gaps < 4 KiB put every byte of the span on a page holding payload bytes; any
   // other order or gap qualifies when the span lies inside one device allocation (the arena's cost follows
   // the span, which the density bound above keeps within 1.5x the payload bytes, in any order).
   const bool any_order = arena && (h.bad || slot->data.prev.bad);
-  if (any_order) arena = range_mapped(b + h.lo, b + h.hi);
   ArenaLaunch a{};
   if (arena) {
     arena_fill_range(c, d_base, b + h.lo, b + h.hi, a);
@@ -816,10 +852,19 @@ int run_var_auto(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_o
     }
     slot->data.since_extent = 0;
   }
+  // No verdict from two records yet, and no record against the arena: the device chooses (AutoChoice) from this
+  // call's own extent - so a caller that passes fresh offset/length arrays on every call (per-connection batches)
+  // still reaches the arena path. A completed record for these pointers that rules the arena out
+  // (sparse, or unsorted across allocations) sends the call to the sorted path directly.
+  const bool device = !arena && !(have1 && !allow_h);
+  if (device) {
+    const size_t want = std::max<size_t>(sorted_scratch_bytes(n), (size_t)slot->data.arena_want);
+    if ((rc = scratch_slot(c, stream, want, &slot))) return rc;
+  }
   // this call's extent: the check the arena launches make, and the next calls' record (on the sorted
   // path the bucket count runs in the same launch, and the bucket place publishes the record)
   const uint64_t seq = ++slot->data.calls;
-  (arena ? c.auto_arena : c.auto_sorted)++;
+  (arena ? c.auto_arena : device ? c.auto_device : c.auto_sorted)++;
   if (arena) {
     uint32_t parts = 0;
     hipError_t e = launch_extent(d_off, d_len, n, slot->data.ptr, &parts, nullptr, stream);
@@ -832,6 +877,33 @@ int run_var_auto(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_o
       e = launch_arena(a, stream);
     }
     rc = e == hipSuccess ? ANNETY_CRC_OK : hip_fail(e);
+  } else if (device) {
+    // extent partials, then both paths' launches; each runs only if the device's choice is its own, and the one that
+    // runs publishes the record
+    uint32_t parts = 0;
+    hipError_t e = launch_extent(d_off, d_len, n, slot->data.ptr, &parts, nullptr, stream);
+    AutoChoice ch{};
+    ch.ws = static_cast<const uint64_t*>(slot->data.ptr);
+    ch.parts = parts;
+    ch.blocks = (uint32_t)grid_cus(c);
+    ch.base = b;
+    ch.cap_words = slot->data.bytes / sizeof(uint32_t);
+    if (e == hipSuccess) {
+      arena_fill_range(c, d_base, 0, 0, a);  // (images and grid; the span is the device's)
+      a.off = d_off;
+      a.len = d_len;
+      a.n = n;
+      a.out = d_out;
+      a.update = update;
+      a.record = slot->data.hint;
+      a.record_seq = seq;
+      a.scratch = reinterpret_cast<uint32_t*>(path_scratch(slot));
+      a.choice = ch;
+      e = launch_arena(a, stream);
+    }
+    rc = e == hipSuccess ? run_var_sorted_in(c, slot, d_base, n, d_off, d_len, d_out, stream, update, slot->data.hint,
+                                             seq, &ch)
+                         : hip_fail(e);
   } else {
     rc = run_var_sorted_in(c, slot, d_base, n, d_off, d_len, d_out, stream, update, slot->data.hint, seq);
   }
@@ -1061,11 +1133,13 @@ int annety_crc_set_var_path(int mode) {
 
 int annety_crc_get_var_path(void) { return g_var_mode.load(); }
 
-int annety_crc_var_path_stats(int device, uint64_t* arena, uint64_t* sorted, uint64_t* arena_unrecorded) {
+int annety_crc_var_path_stats(int device, uint64_t* arena, uint64_t* sorted, uint64_t* arena_unrecorded,
+                              uint64_t* device_chosen) {
   if (device < 0 || device >= kMaxDev) return ANNETY_CRC_ENODEV;
   if (arena) *arena = g_dev[device].auto_arena.load();
   if (sorted) *sorted = g_dev[device].auto_sorted.load();
   if (arena_unrecorded) *arena_unrecorded = g_dev[device].auto_unchecked.load();
+  if (device_chosen) *device_chosen = g_dev[device].auto_device.load();
   return ANNETY_CRC_OK;
 }
 

@@ -6,6 +6,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include "crc32_kernels.h"
 #include "crc32_math.h"
 
 namespace annety_crc {
@@ -402,6 +403,49 @@ __device__ __forceinline__ uint32_t sb_join(uint32_t s, const uint32_t* lds, uin
 #pragma unroll
   for (int k = 0; k < 8; k++) r[k] = t[k * 128 + __builtin_amdgcn_ubfe(s, 4 * k, 4) * 8];
   return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6] ^ r[7]);
+}
+
+// This call's extent from the launch_extent partials (ws + 8 + 4b: {lo, hi, sum, bad} of block b), reduced
+// by the calling wave; every wave computes the same values.
+__device__ __forceinline__ void extent_of(const uint64_t* ws, uint32_t parts, uint64_t& lo, uint64_t& hi,
+                                          uint64_t& sum, uint64_t& bad) {
+  lo = ~0ull;
+  hi = sum = bad = 0;
+  for (uint32_t b = threadIdx.x & 63; b < parts; b += 64) {
+    const uint64_t* q = ws + 8 + 4 * (size_t)b;
+    lo = min(lo, q[0]);
+    hi = max(hi, q[1]);
+    sum += q[2];
+    bad |= q[3];
+  }
+#pragma unroll
+  for (int d = 32; d >= 1; d >>= 1) {
+    lo = min(lo, (uint64_t)__shfl_xor((unsigned long long)lo, d));
+    hi = max(hi, (uint64_t)__shfl_xor((unsigned long long)hi, d));
+    sum += (uint64_t)__shfl_xor((unsigned long long)sum, d);
+    bad |= (uint64_t)__shfl_xor((unsigned long long)bad, d);
+  }
+}
+
+// AutoChoice (crc32_kernels.h): true if the device picks the arena path for this call, with sp = the span of the
+// batch's payload bytes. Called by whole waves (extent_of reduces across the wave); every wave of every launch of
+// the call gets the same answer from the same partials.
+__device__ __forceinline__ bool choose_arena(const AutoChoice& c, ArenaSpan& sp) {
+  uint64_t lo, hi, sum, bad;
+  extent_of(c.ws, c.parts, lo, hi, sum, bad);
+  // (wave-uniform after the reduction: into scalar registers, so the span and the geometry derived from it stay
+  // out of the VGPRs of the kernels that use them)
+  auto uni = [](uint64_t x) {
+    return ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(x >> 32)) << 32) |
+           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)x);
+  };
+  lo = uni(lo);
+  hi = uni(hi);
+  sum = uni(sum);
+  bad = uni(bad);
+  if (!(sum > 0 && hi > lo && bad == 0 && sum * 3 >= (hi - lo) * 2 && hi - lo < (32ull << 30))) return false;
+  sp = arena_span(c.base + lo, c.base + hi);
+  return arena_geom_of(sp.fs1 - sp.fs0, c.blocks).words <= c.cap_words;
 }
 
 }  // namespace

@@ -26,6 +26,21 @@ struct ShiftCols {
   uint32_t c[32];  // columns of a GF(2) 32x32 matrix (passed by value in the kernarg segment)
 };
 
+// The automatic variable path's choice ON THE DEVICE (annety_crc32_batch_var with offset/length arrays the host has
+// no record for): one call enqueues the extent kernel, then both paths' launches; each launch reduces this call's
+// extent from the extent partials (ws, parts) and runs only if the choice is its own (crc32_device.h choose_arena):
+// the arena path iff the batch is dense (payload bytes >= 2/3 of the span), sorted with gaps < 4 KiB (every byte of
+// the span then lies on a page holding payload bytes) and its scratch fits cap_words; else the sorted path. The
+// arena launches derive their geometry from the span (line pass on `blocks` workgroups). ws == null: no choice
+// (the host chose).
+struct AutoChoice {
+  const uint64_t* ws;  // launch_extent's partials
+  uint32_t parts;
+  uint32_t blocks;     // the arena line pass's workgroups (its grid)
+  uint64_t base;       // the batch's base address (payload offsets are relative to it)
+  uint64_t cap_words;  // scratch words the arena path may use
+};
+
 struct FixedLaunch {
   const void* base;        // device pointer to payload 0 (16-byte aligned)
   size_t n;                // payload count
@@ -60,6 +75,7 @@ struct VarLaunch {
   uint32_t* out;             // digests, or (update) the register array, read and written in place
   size_t max_blocks;
   bool update;               // crc32_update semantics instead of crc32_long
+  AutoChoice choice;         // the sorted kernel: run only if the device chose the sorted path (ws null: always)
 };
 
 hipError_t launch_var(const VarLaunch& a, hipStream_t stream);
@@ -148,6 +164,9 @@ struct ArenaLaunch {
   bool check_any_order;      // the recorded span lies in one allocation: unsorted or gapped batches qualify
   ExtentHint* record;
   uint64_t record_seq;
+  // the device's choice (AutoChoice): the launches run only if it is the arena, with the geometry of this call's span
+  // (byte_lo .. fs1 above are then unused) and `scratch` of choice.cap_words words
+  AutoChoice choice;
 };
 
 // Counting sort of a variable batch by rounds (ceil(128-byte lines / 8)), longest first, for the sorted path:
@@ -184,6 +203,7 @@ struct BucketArgs {
   uint32_t* split_slot;                // n words: 1 when a long payload runs as segments, else 0
   uint32_t* split_state;               // update mode, n words: a split payload's register (SortedSplit::state)
   uint32_t split_cap;                  // extra descriptors this call may claim (<= kSplitSegCap)
+  AutoChoice choice;  // both launches run only if the device chose the sorted path (ws null: always)
 };
 unsigned bucket_grid(size_t n);  // blocks of both launches (= the extent partials: at most kExtentMaxParts)
 
@@ -220,9 +240,8 @@ struct ArenaGeom {
   uint64_t nbursts;      // ceil(ntasks / kSTasks)
   uint64_t sb_off, edge_off, words;
 };
-inline ArenaGeom arena_geom(const ArenaLaunch& a, size_t line_blocks) {  // line_blocks >= 1
+inline __host__ __device__ ArenaGeom arena_geom_of(uint64_t nsbf /* full superblocks */, size_t line_blocks) {
   ArenaGeom g{};
-  const uint64_t nsbf = a.fs1 - a.fs0;  // full superblocks
   g.blocks = line_blocks ? line_blocks : 1;
   g.W = 8 * (uint64_t)g.blocks;
   g.ntasks = (nsbf + g.W - 1) / g.W;
@@ -231,6 +250,26 @@ inline ArenaGeom arena_geom(const ArenaLaunch& a, size_t line_blocks) {  // line
   g.edge_off = g.sb_off + nsbf * 8;
   g.words = g.edge_off + 144;
   return g;
+}
+inline ArenaGeom arena_geom(const ArenaLaunch& a, size_t line_blocks) {  // line_blocks >= 1
+  return arena_geom_of(a.fs1 - a.fs0, line_blocks);
+}
+// The lines and superblocks of the arena [byte_lo, byte_hi) (absolute addresses, byte_hi > byte_lo).
+struct ArenaSpan {
+  uint64_t byte_lo, byte_hi, line_lo, line_hi, sb0, nsb, fs0, fs1;
+};
+inline __host__ __device__ ArenaSpan arena_span(uint64_t byte_lo, uint64_t byte_hi) {
+  ArenaSpan s;
+  s.byte_lo = byte_lo;
+  s.byte_hi = byte_hi;
+  s.line_lo = byte_lo >> 7;
+  s.line_hi = (byte_hi - 1) >> 7;
+  s.sb0 = s.line_lo >> 6;
+  s.nsb = (s.line_hi >> 6) - s.sb0 + 1;
+  s.fs0 = (byte_lo + 8191) >> 13;  // superblocks wholly inside the arena
+  s.fs1 = byte_hi >> 13;
+  if (s.fs1 < s.fs0) s.fs1 = s.fs0;
+  return s;
 }
 // The line pass on min(max_blocks, what the arena fills) workgroups.
 inline ArenaGeom arena_geom(const ArenaLaunch& a) {

@@ -943,9 +943,14 @@ __global__ __launch_bounds__(kW8Block) void crc32_var_sorted_kernel(const uint8_
                                                                   const uint32_t* __restrict__ ranges,
                                                                   const uint4* __restrict__ img_slice,
                                                                   const uint4* __restrict__ img_w8,
-                                                                  uint32_t* __restrict__ out, SortedSplit split) {
+                                                                  uint32_t* __restrict__ out, SortedSplit split,
+                                                                  AutoChoice choice) {
   __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsW8TotalBytes / 16];
   static_assert(kW8Block % 64 == 0 && kW8Block / 64 <= kW8MaxWaves, "the claim rings hold one ring per wave");
+  if (choice.ws) {  // the device's choice (AutoChoice): nothing to do when it is the arena
+    ArenaSpan sp;
+    if (choose_arena(choice, sp)) return;
+  }
   var_class_w8<UPD, PROBE>(lds4, base, desc, ranges, img_slice, img_w8, out, split);
 }
 
@@ -1135,7 +1140,8 @@ hipError_t launch_var_sorted(const VarLaunch& a, const void* img_w8, const Sorte
 #define ANNETY_SORTED_LAUNCH(UPD, PROBE)                                                                      \
   hipLaunchKernelGGL((crc32_var_sorted_kernel<UPD, PROBE>), dim3(blocks), dim3(kW8Block), 0, stream,            \
                      static_cast<const uint8_t*>(a.base), a.n, static_cast<const uint4*>(a.desc), a.range,      \
-                     static_cast<const uint4*>(a.img_slice), static_cast<const uint4*>(img_w8), a.out, split)
+                     static_cast<const uint4*>(a.img_slice), static_cast<const uint4*>(img_w8), a.out, split, \
+                     a.choice)
 #ifdef ANNETY_CRC_AB
   static const int probe = ANNETY_AB_KNOB("ANNETY_CRC_W8_PROBE", 0);
   if (!a.update && probe == 1) ANNETY_SORTED_LAUNCH(false, 1);

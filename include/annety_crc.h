@@ -102,10 +102,12 @@ int annety_crc_scratch_stats(int device, uint64_t* slots, uint64_t* handoffs, ui
  * ANNETY_CRC_EINVAL. Digests do not depend on it. get returns the current mode. */
 int annety_crc_set_var_path(int mode);
 int annety_crc_get_var_path(void);
-/* Calls of annety_crc32_batch_var / annety_crc32_update_batch_var on `device` (n >= 1024) that took the
- * arena path and the sorted path so far (the automatic choice; test and tuning visibility), and how many
- * of the arena calls ran without recording their extent (between two recording calls). Any may be NULL. */
-int annety_crc_var_path_stats(int device, uint64_t* arena, uint64_t* sorted, uint64_t* arena_unrecorded);
+/* Calls of annety_crc32_batch_var / annety_crc32_update_batch_var on `device` (n >= 1024) whose path the host chose
+ * from recorded extents - the arena path (and how many of those ran without recording their extent, between two
+ * recording calls) or the sorted path - and calls whose path the device chose from the call's own extent (test and
+ * tuning visibility). Any pointer may be NULL. */
+int annety_crc_var_path_stats(int device, uint64_t* arena, uint64_t* sorted, uint64_t* arena_unrecorded,
+                              uint64_t* device_chosen);
 
 /* ---- host scalar API: exact replacements of the reference's inline methods ----
  * annety_crc32_long   replaces Crc32c::crc32_long(const char*, size_t)   include/Crc32c.h:58-69
@@ -133,8 +135,12 @@ int annety_crc32_batch_fixed(const void* d_base, size_t n, size_t len, size_t st
  * Path choice is automatic. A recording call runs the extent kernel (a few us), which publishes the batch's
  * extent; once two completed recording calls on the same stream with the same (d_base, d_off, d_len, n) have
  * shown a dense batch (payload bytes >= 2/3 of the span) that is either sorted (starts ascending, gaps < 4 KiB)
- * or lies inside one device allocation (any order, any gaps), calls take the arena path over that span;
- * otherwise (and for n < 1024) the length-sorted path. On the arena path one
+ * or lies inside one device allocation (any order, any gaps), calls take the arena path over that span; once a
+ * completed record for those pointers rules the arena out (sparse, or unsorted across allocations), and for
+ * n < 1024, the length-sorted path. Until then - and on every call of a caller that passes fresh offset / length
+ * arrays each time - the device chooses within the call: after the extent kernel, both paths' launches are
+ * enqueued and only the chosen one runs (the arena iff the batch is dense, sorted with gaps < 4 KiB, and its
+ * scratch fits the stream's, which grows to the densest span recorded on the stream). On the arena path one
  * call in 8 records: it re-checks its own extent on the device and, if the layout changed under the same
  * pointers, folds every payload directly from its own bytes. The 7 calls in between skip the extent kernel
  * and the device check: the span is checked on the host to lie inside one device allocation (so the line

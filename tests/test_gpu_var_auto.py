@@ -1,8 +1,10 @@
 """Automatic path choice of annety_crc32_batch_var / annety_crc32_update_batch_var (crc32_capi.cpp
 run_var_auto): every call records its batch's extent on the device; once two completed calls on a stream
 with the same pointers showed a dense sorted batch the arena path runs, re-checking each call's own extent on
-the device. Digests are checked against the oracle on every call, also when the layout changes under the
-same pointers (the arena launches then fold each payload directly) and for sparse batches (sorted path)."""
+the device. Until the records decide - and on every call with fresh offset/length arrays - the device chooses
+within the call (AutoChoice: extent kernel, then both paths' launches, only the chosen one runs). Digests are
+checked against the oracle on every call, also when the layout changes under the same pointers (the arena
+launches then fold each payload directly) and for sparse batches (sorted path)."""
 import numpy as np
 import pytest
 
@@ -49,7 +51,8 @@ def test_dense_batch_moves_to_arena(gpu):
         annety_amd.crc32_batch_var(d, o, ln, out=out)
         _check(out, data, offs, lens)  # synchronises: this call's extent record is complete
     s1 = annety_amd.var_path_stats(0)
-    assert s1["sorted"] - s0["sorted"] == 2 and s1["arena"] - s0["arena"] == 4, (s0, s1)
+    assert s1["device"] - s0["device"] == 2 and s1["arena"] - s0["arena"] == 4, (s0, s1)
+    assert s1["sorted"] == s0["sorted"], (s0, s1)
     # back to back without waiting: every digest still exact
     outs = [torch.empty(len(lens), dtype=torch.int32, device=gpu) for _ in range(8)]
     for x in outs:
@@ -71,7 +74,8 @@ def test_sparse_batch_stays_sorted(gpu):
         annety_amd.crc32_batch_var(d, o, ln, out=out)
         _check(out, data, offs, lens)
     s1 = annety_amd.var_path_stats(0)
-    assert s1["arena"] == s0["arena"] and s1["sorted"] - s0["sorted"] == 4
+    # the first call's device choice (sorted), then its record sends the rest to the sorted path directly
+    assert s1["arena"] == s0["arena"] and s1["device"] - s0["device"] == 1 and s1["sorted"] - s0["sorted"] == 3
 
 
 def test_layout_changes_under_the_same_pointers(gpu):
@@ -145,7 +149,8 @@ def test_sorted_calls_back_to_back(gpu):
     for (data, offs, lens, _), out in zip(cases, outs):
         _check(out, data, offs, lens)
     s1 = annety_amd.var_path_stats(0)
-    assert s1["arena"] == s0["arena"] and s1["sorted"] - s0["sorted"] == 5, (s0, s1)
+    # every batch is new to the stream: the device chose (the sorted path: sparse, unsorted)
+    assert s1["arena"] == s0["arena"] and s1["device"] - s0["device"] == 5, (s0, s1)
 
 
 def test_unrecorded_arena_calls_between_records(gpu):
@@ -202,7 +207,8 @@ def test_dense_unsorted_or_gapped_batch_moves_to_arena(gpu, layout):
         annety_amd.crc32_batch_var(d, o, ln, out=out)
         _check(out, data, offs, lens)
     s1 = annety_amd.var_path_stats(0)
-    assert s1["sorted"] - s0["sorted"] == 2 and s1["arena"] - s0["arena"] == 10, (s0, s1)
+    # (the device cannot see allocations: it runs these on the sorted path until the host's records decide)
+    assert s1["device"] - s0["device"] == 2 and s1["arena"] - s0["arena"] == 10, (s0, s1)
 
 
 @pytest.mark.parametrize("density,arena", [(0.655, False), (0.680, True)])
@@ -231,6 +237,86 @@ def test_density_boundary_inside_one_allocation(gpu, density, arena):
         _check(out, data, offs, lens)
     s1 = annety_amd.var_path_stats(0)
     if arena:
-        assert s1["sorted"] - s0["sorted"] == 2 and s1["arena"] - s0["arena"] == 4, (s0, s1)
+        assert s1["device"] - s0["device"] == 2 and s1["arena"] - s0["arena"] == 4, (s0, s1)
     else:
-        assert s1["arena"] == s0["arena"] and s1["sorted"] - s0["sorted"] == 6, (s0, s1)
+        assert s1["arena"] == s0["arena"] and s1["device"] - s0["device"] == 1, (s0, s1)
+        assert s1["sorted"] - s0["sorted"] == 5, (s0, s1)
+
+
+def _fresh_calls(gpu, data, offs, lens, calls, update=False):
+    """`calls` calls with fresh offset/length tensors each time (per-connection batches), every result checked;
+    returns the device time of the last call (ms, HIP events) and the stats delta."""
+    import torch
+
+    import annety_amd
+
+    d = torch.from_numpy(data).to(gpu)
+    s0 = annety_amd.var_path_stats(0)
+    ms = None
+    want = np.full(len(lens), 0xFFFFFFFF, dtype=np.uint32)
+    state = torch.full((len(lens),), -1, dtype=torch.int32, device=gpu)
+    keep = []  # every call's arrays stay alive, so no two calls share an address (the caching allocator would reuse)
+    for i in range(calls):
+        o = torch.from_numpy(offs.copy()).to(gpu)
+        ln = torch.from_numpy(lens.astype(np.int32)).to(gpu)
+        out = torch.full((len(lens),), 7, dtype=torch.int32, device=gpu)
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        if update:
+            annety_amd.crc32_update_batch_var(state, d, o, ln)
+        else:
+            annety_amd.crc32_batch_var(d, o, ln, out=out)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1)
+        if update:
+            want = oracle.batch_var_mt(data, offs.astype(np.uint64), lens.astype(np.uint32), threads=16, states=want)
+            assert np.array_equal(state.cpu().numpy().view(np.uint32), want)
+        else:
+            want = oracle.batch_var_mt(data, offs.astype(np.uint64), lens.astype(np.uint32), threads=16)
+            assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
+        keep.append((o, ln, out))
+    s1 = annety_amd.var_path_stats(0)
+    return ms, {k: s1[k] - s0[k] for k in s1}
+
+
+def _small_frames(seed, n):
+    """n LengthHeaderCodec-like payloads of 16 B-1 KiB packed with 8-byte gaps (a received frame stream)."""
+    rng = np.random.default_rng(seed)
+    lens = rng.integers(16, 1025, n).astype(np.int64)
+    offs = (np.concatenate([[0], np.cumsum(lens + 8)[:-1]]) + 4).astype(np.int64)
+    data = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 260, dtype=np.uint8)
+    return data, offs, lens
+
+
+def test_fresh_pointers_reach_the_arena(gpu):
+    """a caller passing new offset/length tensors on every call never has two records for the
+    same pointers, so only the device's choice can take it to the arena path. 2M small frames: the sorted path
+    takes ~457 us, the arena ~284 us; each call here must be on the arena's side (the first call may run sorted
+    while the stream's scratch grows to the recorded span)."""
+    import annety_amd
+
+    data, offs, lens = _small_frames(21, 2 << 20)
+    ms, st = _fresh_calls(gpu, data, offs, lens, 4)
+    prev = annety_amd.set_var_path("sorted")
+    try:
+        ms_sorted, _ = _fresh_calls(gpu, data, offs, lens, 2)
+    finally:
+        annety_amd.set_var_path(prev)
+    print(f"2M small frames, fresh pointers per call: {ms * 1e3:.1f} us (sorted path {ms_sorted * 1e3:.1f} us)")
+    assert st["device"] == 4 and st["arena"] == 0 and st["sorted"] == 0, st
+    assert ms < 0.8 * ms_sorted, (ms, ms_sorted)
+
+
+def test_fresh_pointers_update_and_sparse(gpu):
+    """The device choice in update mode (registers carried over calls, fresh pointers each call), and on sparse
+    batches (the device keeps them on the sorted path)."""
+    data, offs, lens = _small_frames(22, 30000)
+    _fresh_calls(gpu, data, offs, lens, 3, update=True)
+    rng = np.random.default_rng(23)
+    lens = rng.integers(0, 3000, 5000).astype(np.int64)
+    offs = np.concatenate([[0], np.cumsum(lens + 20000)[:-1]]).astype(np.int64)
+    data = rng.integers(0, 256, int(offs[-1] + lens[-1]) + 256, dtype=np.uint8)
+    _, st = _fresh_calls(gpu, data, offs, lens, 3)
+    assert st["device"] == 3, st
