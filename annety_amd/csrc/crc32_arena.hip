@@ -48,6 +48,8 @@ namespace {
 // register-pressure-dependent fault we did not pin down)
 constexpr int kStitchBlock = 512;
 constexpr uint32_t kMidChunk = kMidMaps + 1;  // whole superblocks combined per level (P(1..7) and the identity)
+// Runs of more whole superblocks than this (a payload of more than ~512 KiB) are joined by the whole wave (mid_join)
+constexpr uint32_t kLongMid = 64;
 
 // (nibble_map_set: crc32_device.h)
 // shift_{-m} for m in [0, 128): U_hi[m >> 4] o U_lo[m & 15]
@@ -111,6 +113,7 @@ struct StitchGeo {
   ExtentHint* record;
   uint64_t record_seq;
   AutoChoice choice;  // ArenaLaunch::choice: W0 = the scratch, the geometry from the device's span
+  const uint32_t* pow8k;  // ArenaLaunch::pow8k
 };
 
 // The stitch's geometry for the span the device chose (AutoChoice; the host's stitch_geo below).
@@ -327,99 +330,156 @@ struct Stitcher {
     for (uint32_t c = 0; c < kMidChunk; c++) v.mid[c] = word(ma[c]);
   }
 
-  __device__ __forceinline__ void process(size_t p, const Plan& y, Vals& v) const {
-    if (y.len == 0) {  // crc of the empty string is 0; update mode leaves the register alone
-      if constexpr (!UPD) put(p, 0u, v);
-      return;
+  // shift_{m * 8 KiB}(x) from the power table (ArenaLaunch::pow8k; m beyond its reach in several applications)
+  __device__ __forceinline__ uint32_t pow8k(uint32_t x, uint32_t m) const {
+    while (m) {
+      const uint32_t e = m < kSplitMaxSegs - 1 ? m : kSplitMaxSegs - 1;
+      const uint32_t* P = g.pow8k + (size_t)(e - 1) * 32;
+      uint32_t r = 0;
+#pragma unroll 8
+      for (int b = 0; b < 32; b++) r ^= P[b] & (0u - ((x >> b) & 1u));  // (8 loads at a time: few VGPRs)
+      x = r;
+      m -= e;
     }
-    if constexpr (PROBE == 1) {
-      g.out[p] = (uint32_t)y.A ^ y.lead ^ v.s0;
-      return;
-    }
-    if constexpr (PROBE == 2) {
-      uint32_t t = v.s0;
+    return x;
+  }
+
+  // The whole superblocks between a payload's partial ones (y.nmid of them from y.mid_s): acc = V before them ->
+  // V after them = shift_{n 8KiB}(acc) ^ xor_q shift_{(n-1-q) 8KiB}(SB[q, 0]). Runs of up to kLongMid superblocks
+  // are a chain of shift_8KiB steps on the payload's lane; longer runs (a payload of more than ~512 KiB; up to 8k
+  // superblocks for one of the codec's 64 MiB frames) are taken by the whole wave, one run after another: lane l
+  // chains its 1/64 of the run, its share enters as shift_{(superblocks after it) 8KiB} from the power table, and a
+  // wave reduction gives the run's lane V after it (the chain was serial). Called by every lane
+  // of the wave; `on`: this lane's payload has a run to join.
+  __device__ __forceinline__ uint32_t mid_join(uint32_t acc, bool on, const Plan& y, Vals& v) const {
+    const bool lng = on && y.nmid > kLongMid;
+    if (on && !lng && y.nmid) {
+      if constexpr (MID) {
+        acc = mid_level(acc, y.nmid < kMidChunk ? y.nmid : kMidChunk, v.mid);
+        for (uint32_t i = kMidChunk; i < y.nmid; i += kMidChunk) {
+          const uint32_t cnt = y.nmid - i < kMidChunk ? y.nmid - i : kMidChunk;
+          uint32_t ma[kMidChunk], w[kMidChunk];
+          mid_addrs(y.mid_s + i, cnt, ma);
 #pragma unroll
-      for (int q = 0; q < 4; q++) t ^= v.h[q].x ^ v.t[q].y ^ v.x[q] ^ v.y[q];
-#pragma unroll
-      for (uint32_t c = 0; c < kMidChunk; c++) t ^= v.mid[c];
-      g.out[p] = t;
-      return;
-    }
-    uint32_t acc;
-    if (y.fast) {
-      mask_line<4>(v.h, (int32_t)y.hlo * 8, (int32_t)y.hhi * 8);
-      mask_line<4>(v.t, (int32_t)y.tlo * 8, (int32_t)y.thi * 8);
-      uint32_t wh, wt;
-      absorb_two_windows(v.h, v.t, k, lds, wh, wt);
-      // head: V(first line start) = shift_{-lead}(s0) ^ shift_{-64}(wh), or
-      //       V(first line end) = shift_{-lead}(shift_128(s0)) ^ wh
-      const uint32_t f1s = seg_map(v.s0, kMapF, lds);
-      const uint32_t u64 = nibble_map_set<8>(wh, lds, kLdsStitchUnshiftOff + 8192, 4);  // shift_{-64}
-      acc = unshift(y.headX ? v.s0 : f1s, y.lead, lds) ^ (y.headX ? u64 : wh);
-      if constexpr (PROBE != 3) {
-#pragma unroll
-        for (int q = 0; q < 2; q++) {
-          if ((y.act >> q) & 1u) {
-            const uint32_t d = v.x[q] ^ (((y.yzero >> q) & 1u) ? 0u : v.y[q]);
-            acc = seg_map(acc, __builtin_amdgcn_ubfe(y.m1, 8 * q, 5), lds) ^
-                  seg_map(d, __builtin_amdgcn_ubfe(y.m2, 8 * q, 5), lds);
-          }
+          for (uint32_t c = 0; c < kMidChunk; c++) w[c] = word(ma[c]);
+          acc = mid_level(acc, cnt, w);
         }
-        // whole superblocks between the partial ones, in one level per kMidChunk of them (the first chunk's
-        // words were loaded with the plan; payloads past 7 whole superblocks load the next chunks here)
-        if constexpr (MID) {
-          if (y.nmid) {
-            acc = mid_level(acc, y.nmid < kMidChunk ? y.nmid : kMidChunk, v.mid);
-            for (uint32_t i = kMidChunk; i < y.nmid; i += kMidChunk) {
-              const uint32_t cnt = y.nmid - i < kMidChunk ? y.nmid - i : kMidChunk;
-              uint32_t ma[kMidChunk], w[kMidChunk];
-              mid_addrs(y.mid_s + i, cnt, ma);
+      } else {  // acc = shift_8KiB(acc) ^ SB[s, 0], superblock by superblock
+        for (uint32_t i = 0; i < y.nmid; i += kMidChunk) {
+          if (i > 0) {
+            uint32_t ma[kMidChunk];
+            mid_addrs(y.mid_s + i, y.nmid - i < kMidChunk ? y.nmid - i : kMidChunk, ma);
 #pragma unroll
-              for (uint32_t c = 0; c < kMidChunk; c++) w[c] = word(ma[c]);
-              acc = mid_level(acc, cnt, w);
-            }
+            for (uint32_t c = 0; c < kMidChunk; c++) v.mid[c] = word(ma[c]);
           }
-        } else {  // acc = shift_8KiB(acc) ^ SB[s, 0], superblock by superblock
-          for (uint32_t i = 0; i < y.nmid; i += kMidChunk) {
-            if (i > 0) {
-              uint32_t ma[kMidChunk];
-              mid_addrs(y.mid_s + i, y.nmid - i < kMidChunk ? y.nmid - i : kMidChunk, ma);
 #pragma unroll
-              for (uint32_t c = 0; c < kMidChunk; c++) v.mid[c] = word(ma[c]);
-            }
-#pragma unroll
-            for (uint32_t c = 0; c < kMidChunk; c++)
-              if (i + c < y.nmid) acc = seg_map(acc, kMapG + 7, lds) ^ v.mid[c];
-          }
-        }
-#pragma unroll
-        for (int q = 2; q < 4; q++) {
-          if ((y.act >> q) & 1u) {
-            const uint32_t d = v.x[q] ^ (((y.yzero >> q) & 1u) ? 0u : v.y[q]);
-            acc = seg_map(acc, __builtin_amdgcn_ubfe(y.m1, 8 * q, 5), lds) ^
-                  seg_map(d, __builtin_amdgcn_ubfe(y.m2, 8 * q, 5), lds);
-          }
+          for (uint32_t c = 0; c < kMidChunk; c++)
+            if (i + c < y.nmid) acc = seg_map(acc, kMapG + 7, lds) ^ v.mid[c];
         }
       }
-      // tail: V(E) = shift_{-(128-te)}(V(last line end) ^ wt), or
-      //       shift_{-(128-te)}(shift_128(V(last line start)) ^ shift_64(wt))
-      const uint32_t f1a = seg_map(acc, kMapF, lds);
-      const uint32_t h64 = nibble_map_uniform(wt, lds, kLdsHalfOff);
-      acc = unshift(y.tailX ? acc ^ wt : f1a ^ h64, 128 - y.te, lds);
-    } else {
-      // payload reaches outside the arena the caller declared (or there is none): fold its lines directly
-      const uint64_t L0 = y.A >> 7, L1 = (y.E - 1) >> 7;
-      acc = unshift(v.s0, y.lead, lds);  // V(first line start): the lead bytes are zeros here
-      for (uint64_t i = L0; i <= L1; i++) {
-        uint4 u[8];
-#pragma unroll
-        for (int q = 0; q < 8; q++) u[q] = gload16((i << 7) + 16 * q);
-        mask_line<8>(u, i == L0 ? (int32_t)y.lead * 8 : 0, i == L1 ? (int32_t)y.te * 8 : 1024);
-        const uint32_t r = absorb_line(0u, u, k, lds);
-        acc = seg_map(acc, kMapF, lds) ^ r;
-      }
-      acc = unshift(acc, 128 - y.te, lds);  // drop the zero bytes after the payload end
     }
+    uint64_t todo = __builtin_amdgcn_ballot_w64(lng);
+    const uint32_t l = threadIdx.x & 63;
+    while (todo) {
+      const int src = __builtin_ffsll((long long)todo) - 1;
+      todo &= todo - 1;
+      const uint32_t n = (uint32_t)__builtin_amdgcn_readlane((int)y.nmid, src);
+      const uint32_t ms = (uint32_t)__builtin_amdgcn_readlane((int)y.mid_s, src);
+      const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)acc, src);
+      // (whole superblocks between two partial ones are never the arena's edge ones: SB at sb_word + 8 (sb - fs0))
+      const uint32_t w0 = g.sb_word + (uint32_t)(g.sb0 + ms - g.fs0) * 8;
+      const uint32_t per = (n + 63) / 64, lo = min(n, l * per), hi = min(n, lo + per);
+      uint32_t r = 0;
+      for (uint32_t q = lo; q < hi; q += 4) {  // 4 loads in flight, then their 4 steps
+        uint32_t w[4];
+#pragma unroll
+        for (uint32_t c = 0; c < 4; c++) w[c] = word(q + c < hi ? w0 + 8 * (q + c) : 0u);
+#pragma unroll
+        for (uint32_t c = 0; c < 4; c++)
+          if (q + c < hi) r = seg_map(r, kMapG + 7, lds) ^ w[c];
+      }
+      uint32_t x = pow8k(r, n - hi);   // this lane's share, seen from the run's end
+      if (l == 0) x ^= pow8k(a0, n);  // the register before the run
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) x ^= (uint32_t)__shfl_xor((int)x, o, 64);
+      if (l == (uint32_t)src) acc = x;
+    }
+    return acc;
+  }
+
+  // Payload p's digest (or register). Called by every lane of the wave (mid_join takes the wave); `on`: the lane has
+  // payload p (its plan in y, v).
+  __device__ __forceinline__ void process(size_t p, const Plan& y, Vals& v, bool on) const {
+    bool live = false;  // a payload on the arena path, to finish after the whole superblocks
+    uint32_t acc = 0, wt = 0;
+    if (on) {
+      if (y.len == 0) {  // crc of the empty string is 0; update mode leaves the register alone
+        if constexpr (!UPD) put(p, 0u, v);
+      } else if constexpr (PROBE == 1) {
+        g.out[p] = (uint32_t)y.A ^ y.lead ^ v.s0;
+      } else if constexpr (PROBE == 2) {
+        uint32_t t = v.s0;
+#pragma unroll
+        for (int q = 0; q < 4; q++) t ^= v.h[q].x ^ v.t[q].y ^ v.x[q] ^ v.y[q];
+#pragma unroll
+        for (uint32_t c = 0; c < kMidChunk; c++) t ^= v.mid[c];
+        g.out[p] = t;
+      } else if (y.fast) {
+        live = true;
+        mask_line<4>(v.h, (int32_t)y.hlo * 8, (int32_t)y.hhi * 8);
+        mask_line<4>(v.t, (int32_t)y.tlo * 8, (int32_t)y.thi * 8);
+        uint32_t wh;
+        absorb_two_windows(v.h, v.t, k, lds, wh, wt);
+        // head: V(first line start) = shift_{-lead}(s0) ^ shift_{-64}(wh), or
+        //       V(first line end) = shift_{-lead}(shift_128(s0)) ^ wh
+        const uint32_t f1s = seg_map(v.s0, kMapF, lds);
+        const uint32_t u64 = nibble_map_set<8>(wh, lds, kLdsStitchUnshiftOff + 8192, 4);  // shift_{-64}
+        acc = unshift(y.headX ? v.s0 : f1s, y.lead, lds) ^ (y.headX ? u64 : wh);
+        if constexpr (PROBE != 3) {
+#pragma unroll
+          for (int q = 0; q < 2; q++) {
+            if ((y.act >> q) & 1u) {
+              const uint32_t d = v.x[q] ^ (((y.yzero >> q) & 1u) ? 0u : v.y[q]);
+              acc = seg_map(acc, __builtin_amdgcn_ubfe(y.m1, 8 * q, 5), lds) ^
+                    seg_map(d, __builtin_amdgcn_ubfe(y.m2, 8 * q, 5), lds);
+            }
+          }
+        }
+      } else {
+        // payload reaches outside the arena the caller declared (or there is none): fold its lines directly
+        const uint64_t L0 = y.A >> 7, L1 = (y.E - 1) >> 7;
+        acc = unshift(v.s0, y.lead, lds);  // V(first line start): the lead bytes are zeros here
+        for (uint64_t i = L0; i <= L1; i++) {
+          uint4 u[8];
+#pragma unroll
+          for (int q = 0; q < 8; q++) u[q] = gload16((i << 7) + 16 * q);
+          mask_line<8>(u, i == L0 ? (int32_t)y.lead * 8 : 0, i == L1 ? (int32_t)y.te * 8 : 1024);
+          const uint32_t r = absorb_line(0u, u, k, lds);
+          acc = seg_map(acc, kMapF, lds) ^ r;
+        }
+        acc = unshift(acc, 128 - y.te, lds);  // drop the zero bytes after the payload end
+        put(p, UPD ? acc : ~acc, v);
+      }
+    }
+    // whole superblocks between the partial ones, in one level per kMidChunk of them (the first chunk's words were
+    // loaded with the plan; payloads past 7 whole superblocks load the next chunks here), long runs by the wave
+    if constexpr (PROBE != 3) acc = mid_join(acc, live, y, v);
+    if (!live) return;
+    if constexpr (PROBE != 3) {
+#pragma unroll
+      for (int q = 2; q < 4; q++) {
+        if ((y.act >> q) & 1u) {
+          const uint32_t d = v.x[q] ^ (((y.yzero >> q) & 1u) ? 0u : v.y[q]);
+          acc = seg_map(acc, __builtin_amdgcn_ubfe(y.m1, 8 * q, 5), lds) ^
+                seg_map(d, __builtin_amdgcn_ubfe(y.m2, 8 * q, 5), lds);
+        }
+      }
+    }
+    // tail: V(E) = shift_{-(128-te)}(V(last line end) ^ wt), or
+    //       shift_{-(128-te)}(shift_128(V(last line start)) ^ shift_64(wt))
+    const uint32_t f1a = seg_map(acc, kMapF, lds);
+    const uint32_t h64 = nibble_map_uniform(wt, lds, kLdsHalfOff);
+    acc = unshift(y.tailX ? acc ^ wt : f1a ^ h64, 128 - y.te, lds);
     put(p, UPD ? acc : ~acc, v);
   }
 };
@@ -488,14 +548,15 @@ __global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchGeo g0, c
     }
     load_image<kLdsStitchImageBytes, BLK, kLdsCommonBytes>(lds4, img_slice, nullptr, img_stitch);
     __syncthreads();
-    // (y, v) holds payload p, (y2, v2) payload p + BLK; each refills while the other folds
-    for (size_t p = p_first; p < p_end; p += 2 * BLK) {
-      st.process(p, y, v);
+    // (y, v) holds payload p, (y2, v2) payload p + BLK; each refills while the other folds. Wave-uniform loop:
+    // process() takes the whole wave for long payloads' superblock runs
+    for (size_t p = p_first; __builtin_amdgcn_ballot_w64(p < p_end) != 0; p += 2 * BLK) {
+      st.process(p, y, v, p < p_end);
       if (p + 2 * BLK < p_end) {
         st.plan_a(p + 2 * BLK, y, v);
         st.plan_b(p + 2 * BLK, y, v);
       }
-      if (p + BLK < p_end) st.process(p + BLK, y2, v2);
+      st.process(p + BLK, y2, v2, p + BLK < p_end);
       if (p + 3 * BLK < p_end) {
         st.plan_a(p + 3 * BLK, y2, v2);
         st.plan_b(p + 3 * BLK, y2, v2);
@@ -518,22 +579,24 @@ __global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchGeo g0, c
     st.plan_b(q2, y2, v2);
     load_image<kLdsStitchImageBytes, BLK, kLdsCommonBytes>(lds4, img_slice, nullptr, img_stitch);
     __syncthreads();
-    if (p_first < p_end) st.process(p_first, y, v);
-    if (p2 < p_end) st.process(p2, y2, v2);
-    for (size_t p = p2 + BLK; p < p_end; p += BLK) {
-      st.plan_a(p, y, v);
-      st.plan_b(p, y, v);
-      st.process(p, y, v);
+    st.process(p_first, y, v, p_first < p_end);
+    st.process(p2, y2, v2, p2 < p_end);
+    for (size_t p = p2 + BLK; __builtin_amdgcn_ballot_w64(p < p_end) != 0; p += BLK) {
+      if (p < p_end) {
+        st.plan_a(p, y, v);
+        st.plan_b(p, y, v);
+      }
+      st.process(p, y, v, p < p_end);
     }
   } else {
     load_image<kLdsStitchImageBytes, BLK, kLdsCommonBytes>(lds4, img_slice, nullptr, img_stitch);
     __syncthreads();
-    for (size_t p = p_first; p < p_end; p += BLK) {
-      if (p != p_first) {
+    for (size_t p = p_first; __builtin_amdgcn_ballot_w64(p < p_end) != 0; p += BLK) {
+      if (p != p_first && p < p_end) {
         st.plan_a(p, y, v);
         st.plan_b(p, y, v);
       }
-      st.process(p, y, v);
+      st.process(p, y, v, p < p_end);
     }
   }
 }
@@ -880,6 +943,7 @@ StitchGeo stitch_geo(const ArenaLaunch& a, const ArenaGeom& geo) {
   s.record = a.record;
   s.record_seq = a.record_seq;
   s.choice = a.choice;  // (with a device choice the kernel derives the geometry from W0 = the scratch)
+  s.pow8k = static_cast<const uint32_t*>(a.pow8k);
   return s;
 }
 

@@ -689,10 +689,19 @@ void arena_fill(const DeviceCtx& c, const void* d_base, size_t arena_bytes, Aren
 
 // d_ok: LengthHeaderCodec verify - the stitch compares every digest with the trailer after its payload and writes
 // the verdicts (d_out may then be null: no digests)
+// The stitch's power table for long runs of whole superblocks (ArenaLaunch::pow8k), built once per device.
+int arena_powers(DeviceCtx& c, ArenaLaunch& a) {
+  const uint32_t* p = nullptr;
+  const int rc = split_powers(c, 8192, &p);
+  a.pow8k = p;
+  return rc;
+}
+
 int run_arena(DeviceCtx& c, const void* d_base, size_t arena_bytes, const uint64_t* d_off, const uint32_t* d_len,
               size_t n, uint32_t* d_out, hipStream_t stream, bool update, uint8_t* d_ok = nullptr) {
   ArenaLaunch a{};
   arena_fill(c, d_base, arena_bytes, a);
+  if (const int pr = arena_powers(c, a)) return pr;
   a.off = d_off;
   a.len = d_len;
   a.n = n;
@@ -829,6 +838,7 @@ int run_var_auto(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_o
   // the span, which the density bound above keeps within 1.5x the payload bytes, in any order).
   const bool any_order = arena && (h.bad || slot->data.prev.bad);
   ArenaLaunch a{};
+  if ((rc = arena_powers(c, a))) return rc;
   if (arena) {
     arena_fill_range(c, d_base, b + h.lo, b + h.hi, a);
     a.off = d_off;
@@ -889,7 +899,7 @@ int run_var_auto(DeviceCtx& c, const void* d_base, size_t n, const uint64_t* d_o
     ch.base = b;
     ch.cap_words = slot->data.bytes / sizeof(uint32_t);
     if (e == hipSuccess) {
-      arena_fill_range(c, d_base, 0, 0, a);  // (images and grid; the span is the device's)
+      arena_fill_range(c, d_base, 0, 0, a);  // (images and grid; the span is the device's; a.pow8k set above)
       a.off = d_off;
       a.len = d_len;
       a.n = n;

@@ -167,6 +167,8 @@ struct ArenaLaunch {
   // the device's choice (AutoChoice): the launches run only if it is the arena, with the geometry of this call's span
   // (byte_lo .. fs1 above are then unused) and `scratch` of choice.cap_words words
   AutoChoice choice;
+  // pow8k[(m-1)*32 + bit] = shift_{m*8KiB}(1 << bit), m = 1..kSplitMaxSegs-1: the stitch's long superblock runs
+  const void* pow8k;
 };
 
 // Counting sort of a variable batch by rounds (ceil(128-byte lines / 8)), longest first, for the sorted path:

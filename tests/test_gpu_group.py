@@ -102,7 +102,8 @@ def test_bench_dist_path_one_rank(gpu):
     assert line["gather"]["chunks"] == 1 and line["n_gpus"] == 1 and line["value"] > 0
     assert line["config"]["workload"] == one["config"]["workload"]
     assert line["metric"] == one["metric"] and line["scaling"] == one["scaling"] == "weak"
-    assert one["ms_per_step_min"] <= one["ms_per_step_median"] <= one["ms_per_step_max"]
+    sp = one["step_spread"]
+    assert sp["min_ms"] <= sp["median_ms"] <= sp["max_ms"] and sp["groups"] * sp["steps_per_group"] <= one["steps"]
     c4 = _bench("--dist", "--config", "4", "--payloads", "65536", "--chunks", "3")
     assert c4["gather"]["chunks"] == 3 and c4["gather"]["verified"] is True and "config 4" in c4["metric"]
 
