@@ -42,14 +42,31 @@ def up_to_date() -> bool:
     return all(os.path.getmtime(f) <= t for f in _inputs())
 
 
-def source_digest() -> str:
-    """sha256 (16 hex digits) over the product library's sources and headers (kernels, launchers, C-ABI): what a
-    committed measurement of the kernels (profiles/pmc.py) is stamped with, and what bench.py checks before it
-    reports that measurement as the traffic of the kernels it runs."""
+# The translation unit that holds each product kernel (by name prefix), for the per-unit source digests below.
+KERNEL_UNITS = (("lhc_", "crc32_frames.hip"), ("crc32_arena_", "crc32_arena.hip"),
+                ("crc32_extent_kernel", "crc32_arena.hip"), ("crc32_bucket_place", "crc32_arena.hip"),
+                ("crc32_", "crc32_kernels.hip"))
+
+
+def kernel_unit(kernel: str) -> str:
+    """The .hip file that defines `kernel` (a name as rocprofv3 or annety_crc_last_kernels reports it)."""
+    k = kernel.replace("void ", "").replace("annety_crc::(anonymous namespace)::", "").strip()
+    for prefix, unit in KERNEL_UNITS:
+        if k.startswith(prefix):
+            return unit
+    raise KeyError(kernel)
+
+
+def source_digest(unit: str | None = None) -> str:
+    """sha256 (16 hex digits) over what decides a kernel's code and launches: the kernel's translation unit (`unit`,
+    a .hip file; None = every one), every header and the C-ABI shim that chooses its grids. A committed measurement
+    of the kernels (profiles/pmc.py) carries the digests of the units it measured, and bench.py reports it as the
+    traffic of the kernels it runs only while those digests are the tree's (stale PMC summaries)."""
     import hashlib
 
+    files = [f for f in _inputs() if not f.endswith(".hip") or unit is None or os.path.basename(f) == unit]
     h = hashlib.sha256()
-    for f in sorted(_inputs()):
+    for f in sorted(files):
         h.update(os.path.basename(f).encode() + b"\0")
         with open(f, "rb") as fh:
             h.update(fh.read())

@@ -114,6 +114,9 @@ struct StitchGeo {
   uint64_t record_seq;
   AutoChoice choice;  // ArenaLaunch::choice: W0 = the scratch, the geometry from the device's span
   const uint32_t* pow8k;  // ArenaLaunch::pow8k
+  // lanes per payload: 1, or 64 for batches of few payloads (stitch_spread): a wave per payload, whose 63 other lanes
+  // help with its long superblock runs (mid_join)
+  uint32_t spread;
 };
 
 // The stitch's geometry for the span the device chose (AutoChoice; the host's stitch_geo below).
@@ -347,10 +350,10 @@ struct Stitcher {
   // The whole superblocks between a payload's partial ones (y.nmid of them from y.mid_s): acc = V before them ->
   // V after them = shift_{n 8KiB}(acc) ^ xor_q shift_{(n-1-q) 8KiB}(SB[q, 0]). Runs of up to kLongMid superblocks
   // are a chain of shift_8KiB steps on the payload's lane; longer runs (a payload of more than ~512 KiB; up to 8k
-  // superblocks for one of the codec's 64 MiB frames) are taken by the whole wave, one run after another: lane l
-  // chains its 1/64 of the run, its share enters as shift_{(superblocks after it) 8KiB} from the power table, and a
-  // wave reduction gives the run's lane V after it (the chain was serial). Called by every lane
-  // of the wave; `on`: this lane's payload has a run to join.
+  // superblocks for one of the codec's 64 MiB frames) are taken by all the lanes running this, one run after another:
+  // each chains its share of the run, which enters as shift_{(superblocks after it) 8KiB} from the power table, and a
+  // scalar xor over the lanes gives the run's lane V after it (the chain was serial). `on`: this
+  // lane's payload has a run to join.
   __device__ __forceinline__ uint32_t mid_join(uint32_t acc, bool on, const Plan& y, Vals& v) const {
     const bool lng = on && y.nmid > kLongMid;
     if (on && !lng && y.nmid) {
@@ -378,8 +381,13 @@ struct Stitcher {
         }
       }
     }
-    uint64_t todo = __builtin_amdgcn_ballot_w64(lng);
+    // the lanes running this (the payload loop leaves a wave's last lanes behind at the end of a block's range): they
+    // share each run, rank = this lane's place among them
+    const uint64_t act = __builtin_amdgcn_ballot_w64(true);
+    const uint32_t nact = (uint32_t)__builtin_popcountll(act);
+    const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(act >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)act, 0u));
     const uint32_t l = threadIdx.x & 63;
+    uint64_t todo = __builtin_amdgcn_ballot_w64(lng);
     while (todo) {
       const int src = __builtin_ffsll((long long)todo) - 1;
       todo &= todo - 1;
@@ -388,7 +396,7 @@ struct Stitcher {
       const uint32_t a0 = (uint32_t)__builtin_amdgcn_readlane((int)acc, src);
       // (whole superblocks between two partial ones are never the arena's edge ones: SB at sb_word + 8 (sb - fs0))
       const uint32_t w0 = g.sb_word + (uint32_t)(g.sb0 + ms - g.fs0) * 8;
-      const uint32_t per = (n + 63) / 64, lo = min(n, l * per), hi = min(n, lo + per);
+      const uint32_t per = (n + nact - 1) / nact, lo = min(n, rank * per), hi = min(n, lo + per);
       uint32_t r = 0;
       for (uint32_t q = lo; q < hi; q += 4) {  // 4 loads in flight, then their 4 steps
         uint32_t w[4];
@@ -398,21 +406,22 @@ struct Stitcher {
         for (uint32_t c = 0; c < 4; c++)
           if (q + c < hi) r = seg_map(r, kMapG + 7, lds) ^ w[c];
       }
-      uint32_t x = pow8k(r, n - hi);   // this lane's share, seen from the run's end
-      if (l == 0) x ^= pow8k(a0, n);  // the register before the run
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) x ^= (uint32_t)__shfl_xor((int)x, o, 64);
-      if (l == (uint32_t)src) acc = x;
+      uint32_t x = pow8k(r, n - hi);     // this lane's share, seen from the run's end
+      if (rank == 0) x ^= pow8k(a0, n);  // the register before the run
+      uint32_t tot = 0;                  // xor over the running lanes (scalar: no read of a lane left behind)
+      for (uint64_t m = act; m; m &= m - 1)
+        tot ^= (uint32_t)__builtin_amdgcn_readlane((int)x, __builtin_ffsll((long long)m) - 1);
+      if (l == (uint32_t)src) acc = tot;
     }
     return acc;
   }
 
-  // Payload p's digest (or register). Called by every lane of the wave (mid_join takes the wave); `on`: the lane has
-  // payload p (its plan in y, v).
-  __device__ __forceinline__ void process(size_t p, const Plan& y, Vals& v, bool on) const {
+  // Payload p's digest (or register); mid_join shares long superblock runs among the lanes running this. `own`: this
+  // lane writes the result (with StitchGeo::spread > 1 the payload's other lanes only help with its runs).
+  __device__ __forceinline__ void process(size_t p, const Plan& y, Vals& v, bool own = true) const {
     bool live = false;  // a payload on the arena path, to finish after the whole superblocks
     uint32_t acc = 0, wt = 0;
-    if (on) {
+    if (own) {
       if (y.len == 0) {  // crc of the empty string is 0; update mode leaves the register alone
         if constexpr (!UPD) put(p, 0u, v);
       } else if constexpr (PROBE == 1) {
@@ -532,9 +541,19 @@ __global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchGeo g0, c
   const Stitcher<UPD, PROBE, MID, VER> st{g, reinterpret_cast<const uint32_t*>(lds4), lane_ctx()};
   const size_t per = (g.n + gridDim.x - 1) / gridDim.x;
   const size_t p_end = std::min(g.n, (size_t)(blockIdx.x + 1) * per);
-  const size_t p_first = (size_t)blockIdx.x * per + threadIdx.x;
   Plan y{};
   Vals v{};
+  if (g.spread > 1) {  // a wave per payload (few payloads: the wave helps with its long runs)
+    load_image<kLdsStitchImageBytes, BLK, kLdsCommonBytes>(lds4, img_slice, nullptr, img_stitch);
+    __syncthreads();
+    for (size_t p = (size_t)blockIdx.x * per + threadIdx.x / 64; p < p_end; p += BLK / 64) {
+      st.plan_a(p, y, v);
+      st.plan_b(p, y, v);
+      st.process(p, y, v, (threadIdx.x & 63) == 0);
+    }
+    return;
+  }
+  const size_t p_first = (size_t)blockIdx.x * per + threadIdx.x;
   if (p_first < p_end) {
     st.plan_a(p_first, y, v);
     st.plan_b(p_first, y, v);
@@ -548,15 +567,14 @@ __global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchGeo g0, c
     }
     load_image<kLdsStitchImageBytes, BLK, kLdsCommonBytes>(lds4, img_slice, nullptr, img_stitch);
     __syncthreads();
-    // (y, v) holds payload p, (y2, v2) payload p + BLK; each refills while the other folds. Wave-uniform loop:
-    // process() takes the whole wave for long payloads' superblock runs
-    for (size_t p = p_first; __builtin_amdgcn_ballot_w64(p < p_end) != 0; p += 2 * BLK) {
-      st.process(p, y, v, p < p_end);
+    // (y, v) holds payload p, (y2, v2) payload p + BLK; each refills while the other folds
+    for (size_t p = p_first; p < p_end; p += 2 * BLK) {
+      st.process(p, y, v);
       if (p + 2 * BLK < p_end) {
         st.plan_a(p + 2 * BLK, y, v);
         st.plan_b(p + 2 * BLK, y, v);
       }
-      st.process(p + BLK, y2, v2, p + BLK < p_end);
+      if (p + BLK < p_end) st.process(p + BLK, y2, v2);
       if (p + 3 * BLK < p_end) {
         st.plan_a(p + 3 * BLK, y2, v2);
         st.plan_b(p + 3 * BLK, y2, v2);
@@ -579,24 +597,22 @@ __global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchGeo g0, c
     st.plan_b(q2, y2, v2);
     load_image<kLdsStitchImageBytes, BLK, kLdsCommonBytes>(lds4, img_slice, nullptr, img_stitch);
     __syncthreads();
-    st.process(p_first, y, v, p_first < p_end);
-    st.process(p2, y2, v2, p2 < p_end);
-    for (size_t p = p2 + BLK; __builtin_amdgcn_ballot_w64(p < p_end) != 0; p += BLK) {
-      if (p < p_end) {
-        st.plan_a(p, y, v);
-        st.plan_b(p, y, v);
-      }
-      st.process(p, y, v, p < p_end);
+    if (p_first < p_end) st.process(p_first, y, v);
+    if (p2 < p_end) st.process(p2, y2, v2);
+    for (size_t p = p2 + BLK; p < p_end; p += BLK) {
+      st.plan_a(p, y, v);
+      st.plan_b(p, y, v);
+      st.process(p, y, v);
     }
   } else {
     load_image<kLdsStitchImageBytes, BLK, kLdsCommonBytes>(lds4, img_slice, nullptr, img_stitch);
     __syncthreads();
-    for (size_t p = p_first; __builtin_amdgcn_ballot_w64(p < p_end) != 0; p += BLK) {
-      if (p != p_first && p < p_end) {
+    for (size_t p = p_first; p < p_end; p += BLK) {
+      if (p != p_first) {
         st.plan_a(p, y, v);
         st.plan_b(p, y, v);
       }
-      st.process(p, y, v, p < p_end);
+      st.process(p, y, v);
     }
   }
 }
@@ -905,8 +921,13 @@ LineOut line_out(const ArenaLaunch& a, const ArenaGeom& geo) {
   return ar;
 }
 
+// Lanes per payload in the stitch: a wave each when the batch has few payloads (at most 8 per CU), so that the wave
+// can share a long payload's superblock runs (mid_join; 16 frames of 64 MiB ran their runs on 16 lanes of one wave
+// in ~1.3 ms); one lane each otherwise.
+uint32_t stitch_spread(const ArenaLaunch& a) { return a.n <= a.max_blocks * (kStitchBlock / 64) ? 64u : 1u; }
+
 size_t stitch_blocks(const ArenaLaunch& a, size_t blk = kStitchBlock) {
-  return std::max<size_t>(1, std::min<size_t>(a.max_blocks, (a.n + blk - 1) / blk));
+  return std::max<size_t>(1, std::min<size_t>(a.max_blocks, (a.n * stitch_spread(a) + blk - 1) / blk));
 }
 
 StitchGeo stitch_geo(const ArenaLaunch& a, const ArenaGeom& geo) {
@@ -944,6 +965,7 @@ StitchGeo stitch_geo(const ArenaLaunch& a, const ArenaGeom& geo) {
   s.record_seq = a.record_seq;
   s.choice = a.choice;  // (with a device choice the kernel derives the geometry from W0 = the scratch)
   s.pow8k = static_cast<const uint32_t*>(a.pow8k);
+  s.spread = stitch_spread(a);
   return s;
 }
 

@@ -524,7 +524,7 @@ def pmc_traffic(w: Workload, var_path: str):
     """(per-launch HBM bytes, source file, None) of this workload's kernels from the committed rocprofv3 PMC summary
     (profiles/pmc.sh + pmc.py: FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), summed over the kernels of one step;
     (None, file, reason) when the summary is missing or was measured on other kernel sources than this tree's."""
-    from annety_amd.build import source_digest
+    from annety_amd.build import kernel_unit, source_digest
 
     path = PMC_FILES.get(w.config)
     if w.config == 3 and var_path != "arena":
@@ -538,12 +538,14 @@ def pmc_traffic(w: Workload, var_path: str):
             d = json.load(f)
     except (OSError, ValueError):
         return None, path, "summary missing"
-    have, want = d.get("_meta", {}).get("source_digest"), source_digest()
-    if have != want:
-        return None, path, f"stale: measured on library sources {have}, this tree is {want}"
     # the kernels of one step: the library's own list for it (a summary also holds the setup's launches, e.g. the
     # encode that builds the frames stream of a verify step), by name without template arguments
     step = {x.split("<")[0].strip() for x in (w.kernel or "").split("+") if x.strip()}
+    have = d.get("_meta", {}).get("source_digest") or {}
+    for unit in sorted({kernel_unit(k) for k in step}):
+        if have.get(unit) != source_digest(unit):
+            return None, path, (f"stale: {unit} measured at library sources {have.get(unit)}, this tree is "
+                                f"{source_digest(unit)}")
     tot = sum(v.get("hbm_bytes_per_launch", 0) for k, v in d.items()
               if k != "_meta" and ("crc32_" in k or "lhc_" in k) and (not step or k.split("<")[0].strip() in step))
     if not tot:

@@ -237,7 +237,9 @@ def test_density_boundary_inside_one_allocation(gpu, density, arena):
         _check(out, data, offs, lens)
     s1 = annety_amd.var_path_stats(0)
     if arena:
-        assert s1["device"] - s0["device"] == 2 and s1["arena"] - s0["arena"] == 4, (s0, s1)
+        # (the first call may go to the sorted path on the host's word: torch can hand this test the addresses of the
+        # previous case's tensors, whose records - same pointers, another layout - are not dense)
+        assert s1["device"] + s1["sorted"] - s0["device"] - s0["sorted"] == 2 and s1["arena"] - s0["arena"] == 4, (s0, s1)
     else:
         assert s1["arena"] == s0["arena"] and s1["device"] - s0["device"] == 1, (s0, s1)
         assert s1["sorted"] - s0["sorted"] == 5, (s0, s1)
