@@ -13,6 +13,12 @@ args_of() {
   esac
 }
 for L in "$@"; do
+  if [ "$L" = "e1" ] || [ "$L" = "e3" ]; then  # the host-memory (PCIe) paths of configs 1 and 3
+    C=${L#e}
+    timeout -k 10 600 python3 bench.py --config $C --e2e --no-cpu --steps 50 > $O/bench_e2e_c$C.log 2>&1
+    tail -c 600 $O/bench_e2e_c$C.log
+    continue
+  fi
   A=$(args_of $L)
   echo "== $L: $A"
   if [ "$L" != "c4" ]; then
@@ -20,7 +26,7 @@ for L in "$@"; do
     python3 profiles/pmc.py gpurun_out/pmc_m_$L $O/pmc_$L.json > /dev/null
     find gpurun_out/pmc_m_$L -name "*counter_collection.csv" -delete
   fi
-  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/kt_$L -o run -- \
+  (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $O/kt_$L -o run -- \
      python3 $GRAFT_REPO_ROOT/bench.py $A --no-cpu --sample-check --steps 100 > $O/kt_$L.log 2>&1)
   find $O/kt_$L -name "*kernel_trace.csv" -delete
   if [ "$L" = "c1" ]; then
