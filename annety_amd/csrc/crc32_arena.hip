@@ -523,11 +523,10 @@ __global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchGeo g0, c
     ArenaSpan sp;
     if (!choose_arena(g.choice, sp)) return;
     stitch_geo_chosen(g, sp, arena_geom_of(sp.fs1 - sp.fs0, g.choice.blocks));
-    if (blockIdx.x == 0 && threadIdx.x == 0 && g.record) {  // the next calls' record (crc32_kernels.h)
-      uint64_t lo, hi, sum, bad;
-      extent_of(g.choice.ws, g.choice.parts, lo, hi, sum, bad);
-      publish_extent(g.record, lo, hi, sum, bad, g.record_seq);
-    }
+    // the next calls' record (crc32_kernels.h): extent_of reduces across the wave, so every lane takes part
+    uint64_t lo, hi, sum, bad;
+    extent_of(g.choice.ws, g.choice.parts, lo, hi, sum, bad);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && g.record) publish_extent(g.record, lo, hi, sum, bad, g.record_seq);
   }
   // automatic path: this call's extent, reduced by every wave from the partials; on a mismatch with the
   // declared arena the line pass did nothing, and every payload is folded directly
@@ -727,7 +726,34 @@ __global__ __launch_bounds__(kExtentBlock) void crc32_extent_kernel(const uint64
     __syncthreads();
   }
   uint64_t lo = ~0ull, hi = 0, sum = 0, bad = 0;
-  for (size_t i = blockIdx.x * (size_t)kExtentBlock + threadIdx.x; i < n; i += (size_t)gridDim.x * kExtentBlock) {
+  const size_t stride = (size_t)gridDim.x * kExtentBlock;
+  size_t i = blockIdx.x * (size_t)kExtentBlock + threadIdx.x;
+  if constexpr (!COUNT) {
+    // the extent alone: four payloads' descriptors in flight per thread (one at a time, a 2M-payload batch is 16
+    // dependent rounds per thread on the 128-block grid: ~20 us; crc32_capi.cpp run_var_auto's device choice)
+    for (; i + 3 * stride < n; i += 4 * stride) {
+      uint64_t o[4], nx[4];
+      uint32_t l[4];
+      const bool has_next = i + 3 * stride + 1 < n;  // (only the fourth can be the batch's last payload)
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        o[u] = off[i + u * stride];
+        l[u] = len[i + u * stride];
+        nx[u] = off[u < 3 || has_next ? i + u * stride + 1 : i + u * stride];
+      }
+#pragma unroll
+      for (int u = 0; u < 4; u++) {
+        const bool last = u == 3 && !has_next;
+        if (l[u]) {
+          lo = min(lo, o[u]);
+          hi = max(hi, o[u] + l[u]);
+          sum += l[u];
+        }
+        if (!last) bad |= (nx[u] < o[u] || (nx[u] >= o[u] + l[u] && nx[u] - (o[u] + l[u]) >= 4096)) ? 1u : 0u;
+      }
+    }
+  }
+  for (; i < n; i += stride) {
     const uint64_t o = off[i], l = len[i];
     if (l) {
       lo = min(lo, o);

@@ -309,6 +309,22 @@ def test_fresh_pointers_reach_the_arena(gpu):
     print(f"2M small frames, fresh pointers per call: {ms * 1e3:.1f} us (sorted path {ms_sorted * 1e3:.1f} us)")
     assert st["device"] == 4 and st["arena"] == 0 and st["sorted"] == 0, st
     assert ms < 0.8 * ms_sorted, (ms, ms_sorted)
+    # the records a device-chosen arena call publishes carry the whole batch's extent (every lane of the stitch's
+    # wave reduces the partials): the same pointers again go to the arena path on the host's word from the third call
+    import torch
+
+    d = torch.from_numpy(data).to(gpu)
+    o = torch.from_numpy(offs).to(gpu)
+    ln = torch.from_numpy(lens.astype(np.int32)).to(gpu)
+    out = torch.empty(len(lens), dtype=torch.int32, device=gpu)
+    s0 = annety_amd.var_path_stats(0)
+    for _ in range(5):
+        annety_amd.crc32_batch_var(d, o, ln, out=out)
+        torch.cuda.synchronize()
+    s1 = annety_amd.var_path_stats(0)
+    assert s1["arena"] - s0["arena"] == 3 and s1["device"] - s0["device"] == 2, (s0, s1)
+    want = oracle.batch_var_mt(data, offs.astype(np.uint64), lens.astype(np.uint32), threads=16)
+    assert np.array_equal(out.cpu().numpy().view(np.uint32), want)
 
 
 def test_fresh_pointers_update_and_sparse(gpu):
