@@ -164,7 +164,8 @@ struct Vals {
 // The per-payload stitch (file comment). Phase A issues everything the line pass did not write, phase
 // B the S/SB words.
 //   PROBE (microbench only; product = 0): 1 = descriptors and stores only, 2 = + all loads,
-//   3 = + window folds (no map steps) - wrong digests, used to measure what the stages cost.
+//   3 = + window folds (no map steps), 4 = the product with every S/SB word from one address, 5 = the product with
+//   every window chunk from the zero line - wrong digests, used to measure what the stages cost.
 //   MID (A/B): 1 = the whole superblocks between join in one level (mid_level), 0 = a chain of
 //   dependent shift_8KiB steps.
 //   VER: LengthHeaderCodec verify (LengthHeaderCodec::decode, include/codec/LengthHeaderCodec.h:107-121): the
@@ -260,12 +261,12 @@ struct Stitcher {
     // on average half of each window, which the fold masks to zero anyway
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-      const bool keep = 16u * i < y.hhi && 16u * i + 16 > y.hlo;
+      const bool keep = PROBE != 5 && 16u * i < y.hhi && 16u * i + 16 > y.hlo;
       v.h[i] = gload16((keep ? hsrc : g.zero_line) + 16 * i);
     }
 #pragma unroll
     for (int i = 0; i < 4; i++) {
-      const bool keep = 16u * i < y.thi && 16u * i + 16 > y.tlo;
+      const bool keep = PROBE != 5 && 16u * i < y.thi && 16u * i + 16 > y.tlo;
       v.t[i] = gload16((keep ? tsrc : g.zero_line) + 16 * i);
     }
     v.s0 = UPD ? gload4((uint64_t)(uintptr_t)(g.out + p)) : kInit;
@@ -321,9 +322,24 @@ struct Stitcher {
   // Phase B: the S/SB words of the plan.
   __device__ __forceinline__ void plan_b(size_t /*p*/, const Plan& y, Vals& v) const {
     const uint32_t dummy = 0;  // g.W0[0]: a valid word (the loads of inactive steps are not used)
+    // a wave whose payloads all stay within two blocks (frames, short payloads) has steps 1-2 and the whole
+    // superblocks between empty: it loads only steps 0 and 3 (frames verify 0.290 -> 0.287 ms per step, config 3
+    // unchanged; profiles/r06/abshort/)
+    if (__builtin_amdgcn_ballot_w64((y.act & 6u) != 0 || y.nmid != 0) == 0) {
+#pragma unroll
+      for (int q = 0; q < 4; q += 3) {
+        const bool on = PROBE != 4 && ((y.act >> q) & 1u);
+        v.x[q] = word(on ? y.xa[q] : dummy);
+        v.y[q] = word(on && !((y.yzero >> q) & 1u) ? y.ya[q] : dummy);
+      }
+      v.x[1] = v.x[2] = v.y[1] = v.y[2] = 0;
+#pragma unroll
+      for (uint32_t c = 0; c < kMidChunk; c++) v.mid[c] = 0;
+      return;
+    }
 #pragma unroll
     for (int q = 0; q < 4; q++) {
-      const bool on = (y.act >> q) & 1u;
+      const bool on = PROBE != 4 && ((y.act >> q) & 1u);
       v.x[q] = word(on ? y.xa[q] : dummy);
       v.y[q] = word(on && !((y.yzero >> q) & 1u) ? y.ya[q] : dummy);
     }
@@ -944,6 +960,7 @@ LineOut line_out(const ArenaLaunch& a, const ArenaGeom& geo) {
   ar.check_any_order = a.check_any_order;
   ar.check_hi = a.check_hi;
   ar.choice = a.choice;  // (with a device choice the kernel derives the geometry from S = the scratch)
+  ar.probe_delta = 0;
   return ar;
 }
 
@@ -1068,6 +1085,8 @@ hipError_t launch_arena(const ArenaLaunch& a, hipStream_t stream) {
   if (probe == 1) return launch_stitch_p<1, 1>(a, stream);
   if (probe == 2) return launch_stitch_p<2, 1>(a, stream);
   if (probe == 3) return launch_stitch_p<3, 1>(a, stream);
+  if (probe == 4) return launch_stitch_p<4, 1>(a, stream);
+  if (probe == 5) return launch_stitch_p<5, 1>(a, stream);
   if (mid) return launch_stitch_p<0, 0, kStitchBlock, true>(a, stream);
   if (!pipe) return launch_stitch_p<0>(a, stream);
 #endif

@@ -20,6 +20,7 @@ struct LineOut {
   uint64_t check_lo, check_hi;
   bool check_any_order;
   AutoChoice choice;  // ArenaLaunch::choice: S = the scratch, the rest from the device's span (line_out_chosen)
+  int64_t probe_delta;  // microbench only (PROBE bit 3): each loaded chunk is also stored at its address + this
 };
 
 // The line pass's geometry for the span the device chose (AutoChoice; the host's line_out in crc32_arena.hip).
@@ -51,7 +52,8 @@ __device__ __forceinline__ bool extent_matches(const uint64_t* check, uint32_t p
 }
 
 //   PROBE (microbench only; product = 0): bit 0 drops the S stores, bit 1 the superblock scan, bit 2 only
-//   the SB stores - wrong outputs, used to measure what those stages cost.
+//   the SB stores - wrong outputs, used to measure what those stages cost; bit 3 adds a copy of every loaded chunk
+//   to its address + probe_delta (unaligned 16-byte stores: what a fused copy would cost the pass, microbench/copy_mb).
 // `base` = the first full superblock (fs0 * 8192), passed as its own kernel argument: loads through a
 // __restrict__ kernel-argument pointer compile to the config-1 kernel's schedule; the same loads through
 // integer-built address-space-1 pointers ran this pass 30 % slower (microbench/arena_mb.hip).
@@ -171,6 +173,12 @@ __device__ __forceinline__ void arena_line_pass(const uint8_t* __restrict__ base
   }
 
   auto finish = [&](uint4 (&v)[8], int t) __attribute__((always_inline)) {
+    if constexpr ((PROBE & 8) != 0) {
+      const uint64_t a = (uint64_t)(uintptr_t)base + (g0 + (uint64_t)t * ngroups) * 1024 + coalesced_lane_offset(lane) +
+                         (uint64_t)ar.probe_delta;
+#pragma unroll
+      for (int i = 0; i < 8; i++) gstore16(a + 1024 * i, v[i]);
+    }
     uint32_t r;
     if constexpr (NT) {
       transpose_blocks(v);
