@@ -110,7 +110,25 @@ def build(force: bool = False, verbose: bool = False, ab: bool = False) -> str:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
     os.replace(out_tmp, lib)
+    if not ab:
+        build_native_tests(verbose)
     return lib
+
+
+NATIVE_TESTS = os.path.join(ROOT, "tests", "native")
+
+
+def build_native_tests(verbose: bool = False) -> None:
+    """The GPU test programs that use the C++ headers directly (tests/native/*_device.cpp, run by tests/test_lhc.py),
+    linked against the in-tree library through an $ORIGIN-relative rpath so they run from any checkout."""
+    for src in sorted(f for f in os.listdir(NATIVE_TESTS) if f.endswith("_device.cpp")):
+        exe = os.path.join(NATIVE_TESTS, src[:-4])
+        cmd = ["g++", "-std=c++17", "-O2", "-Wall", "-Wextra", "-Werror", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include",
+               f"-I{INCLUDE}", os.path.join(NATIVE_TESTS, src), "-o", exe, f"-L{PKG}", "-lannety_crc", f"-L{ROCM_LIB}",
+               "-lamdhip64", "-Wl,-rpath,$ORIGIN/../../annety_amd", f"-Wl,-rpath,{ROCM_LIB}"]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
 
 
 if __name__ == "__main__":

@@ -506,3 +506,20 @@ def test_gpu_decode_host_iov_large(frames_pack):
     # a frame cap smaller than the total: later connections report no frames
     capped = codec.decode_host_iov(bufs, max_frames=100)
     assert sum(int(r.ok.size) for r in capped) == 100
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,n", [(1, 3000), (2, 1200), (4, 1200), (8, 300)])
+def test_cpp_batch_codec_device(T, n):
+    """The C++ batch codec's device methods (include/annety/LengthHeaderCodecBatch.h encode/verify) called from C++:
+    tests/native/lhc_batch_device.cpp (built with the library by annety_amd/build.py) encodes a batch on the device
+    with empty and over-long payloads among it, checks every frame byte against the drop-in's host Crc32c, verifies
+    the stream on the device and checks recv_outcome() against Codec::recv, before and after a flipped byte."""
+    import subprocess
+
+    exe = os.path.join(ROOT, "tests", "native", "lhc_batch_device")
+    assert os.path.exists(exe), "tests/native/lhc_batch_device is built by annety_amd/build.py"
+    r = subprocess.run([exe, str(T), str(n), str(17 + T)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.startswith("ok "), r.stdout + r.stderr
+    accepted, total = map(int, r.stdout.split()[1:3])
+    assert accepted > n // 2 and total > 0
