@@ -76,16 +76,20 @@ def source_digest(unit: str | None = None) -> str:
 AB_LIB = os.path.join(ROOT, "microbench", "libannety_crc_ab.so")
 
 
-def build(force: bool = False, verbose: bool = False, ab: bool = False) -> str:
+def build(force: bool = False, verbose: bool = False, ab: bool = False, defines: tuple = (), out: str | None = None) -> str:
     """The product library, or with ab=True the design-space build (-DANNETY_CRC_AB: the A/B and probe switches
     read from the environment, crc32_kernels.h) at microbench/libannety_crc_ab.so, loaded with ANNETY_CRC_LIB.
-    The A/B build is never the product: tests and the bench load LIB."""
-    lib = AB_LIB if ab else LIB
-    if not force and not ab and up_to_date():
+    `defines` (compile-time A/B macros, e.g. ANNETY_S_NT=0) need `out`, a library path of their own. Neither is
+    ever the product: tests and the bench load LIB."""
+    if defines and not out:
+        raise ValueError("a build with extra defines needs its own output path")
+    lib = out or (AB_LIB if ab else LIB)
+    if not force and not ab and not out and up_to_date():
         return LIB
-    tmp = os.path.join(PKG, "build", "ab" if ab else "")
+    tmp = os.path.join(PKG, "build", "ab" if ab else "", "x" if out else "")
     os.makedirs(tmp, exist_ok=True)
     common = ["-std=c++17", "-O3", "-fPIC", f"-I{INCLUDE}", f"-I{CSRC}", "-Wall"] + (["-DANNETY_CRC_AB"] if ab else [])
+    common += [f"-D{d}" for d in defines]
     cmds, objs = [], []
     for s in SOURCES:
         src = os.path.join(CSRC, s)
@@ -110,7 +114,7 @@ def build(force: bool = False, verbose: bool = False, ab: bool = False) -> str:
         print(" ".join(cmd))
     subprocess.run(cmd, check=True)
     os.replace(out_tmp, lib)
-    if not ab:
+    if not ab and not out:
         build_native_tests(verbose)
     return lib
 
@@ -134,4 +138,8 @@ def build_native_tests(verbose: bool = False) -> None:
 if __name__ == "__main__":
     import sys
 
-    print(build(force=True, verbose=True, ab="--ab" in sys.argv))
+    # python -m annety_amd.build [--ab] [-D MACRO=V ... -o path]
+    args = sys.argv[1:]
+    defs = tuple(args[i + 1] for i, a in enumerate(args) if a == "-D")
+    out = args[args.index("-o") + 1] if "-o" in args else None
+    print(build(force=True, verbose=True, ab="--ab" in args, defines=defs, out=out))
