@@ -47,7 +47,7 @@ namespace {
 // returned wrong digests for whole waves now and then on the MI355X with the previous stitch - a
 // register-pressure-dependent fault we did not pin down)
 constexpr int kStitchBlock = 512;
-constexpr uint32_t kMidChunk = kMidMaps + 1;  // whole superblocks combined per level (P(1..7) and the identity)
+constexpr uint32_t kMidChunk = 7;  // whole superblocks between a payload's partial ones whose SB words load with its plan
 // Runs of more whole superblocks than this (a payload of more than ~512 KiB) are joined by the whole wave (mid_join)
 constexpr uint32_t kLongMid = 64;
 
@@ -60,18 +60,6 @@ __device__ __forceinline__ uint32_t unshift(uint32_t t, uint32_t m, const uint32
 __device__ __forceinline__ uint32_t seg_map(uint32_t t, uint32_t idx, const uint32_t* lds) {
   return nibble_map_set<32>(t, lds, kLdsMapOff, idx);
 }
-// P(c) = shift_{c*8KiB} for a lane-varying c in 1..7: G(8) of the segment set for c = 1, else the mid set
-[[maybe_unused]] __device__ __forceinline__ uint32_t mid_map(uint32_t t, uint32_t c, const uint32_t* lds) {
-  const bool one = c == 1;
-  const uint32_t* b = lds + (one ? kLdsMapOff / 4 + (kMapG + 7) * 16 : kLdsMidOff / 4 + (c - 2) * 16);
-  const uint32_t stride = one ? 32 * 16 : kMidMaps * 16;
-  uint32_t r[8];
-#pragma unroll
-  for (int k = 0; k < 8; k++) r[k] = b[k * stride + __builtin_amdgcn_ubfe(t, 4 * k, 4)];
-  return xor3(xor3(r[0], r[1], r[2]), xor3(r[3], r[4], r[5]), r[6] ^ r[7]);
-}
-
-
 // Two 64-byte windows from register 0, four 32-byte chains: raw(window) = shift_32(raw(first half)) ^
 // raw(second half).
 __device__ __forceinline__ void absorb_two_windows(const uint4 (&v)[4], const uint4 (&w)[4], const LaneCtx& k,
@@ -166,12 +154,10 @@ struct Vals {
 //   PROBE (microbench only; product = 0): 1 = descriptors and stores only, 2 = + all loads,
 //   3 = + window folds (no map steps), 4 = the product with every S/SB word from one address, 5 = the product with
 //   every window chunk from the zero line - wrong digests, used to measure what the stages cost.
-//   MID (A/B): 1 = the whole superblocks between join in one level (mid_level), 0 = a chain of
-//   dependent shift_8KiB steps.
 //   VER: LengthHeaderCodec verify (LengthHeaderCodec::decode, include/codec/LengthHeaderCodec.h:107-121): the
 //   4-byte big-endian trailer after each payload is loaded with the plan and compared with the digest here,
 //   ok[p] = 1 on a match (the digest itself is stored only when out is set).
-template <bool UPD, int PROBE, bool MID = false, bool VER = false>
+template <bool UPD, int PROBE, bool VER = false>
 struct Stitcher {
   const StitchGeo& g;
   const uint32_t* lds;
@@ -211,25 +197,12 @@ struct Stitcher {
   }
 
   // SB[., 0] word indices of the whole superblocks mid_s .. mid_s + cnt - 1 (relative to sb0, cnt <= kMidChunk),
-  // the rest 0. MID: last first (a[c] is the superblock that ends c superblocks before the run's end, the term
-  // P(c) shifts); else in order. Whole superblocks between two partial ones are never the arena's edge superblocks, and SB
-  // is linear in the superblock, so no edge selects.
+  // the rest 0. Whole superblocks between two partial ones are never the arena's edge superblocks, and SB is linear
+  // in the superblock, so no edge selects.
   __device__ __forceinline__ void mid_addrs(uint32_t mid_s, uint32_t cnt, uint32_t (&a)[kMidChunk]) const {
     const uint32_t w0 = g.sb_word + (uint32_t)(g.sb0 + mid_s - g.fs0) * 8;
 #pragma unroll
-    for (uint32_t c = 0; c < kMidChunk; c++) a[c] = c < cnt ? w0 + 8 * (MID ? cnt - 1 - c : c) : 0u;
-  }
-
-  // acc = P(cnt)(acc) ^ xor_c P(c)(w[c]) for cnt in 1..kMidChunk, P(c) = shift_{c*8KiB}: cnt whole superblocks
-  // (w[c] = SB[last - c, 0]) joined in one level of independent lookups instead of a chain of cnt dependent
-  // shift_8KiB steps
-  __device__ __forceinline__ uint32_t mid_level(uint32_t acc, uint32_t cnt, const uint32_t (&w)[kMidChunk]) const {
-    uint32_t t = mid_map(acc, cnt, lds) ^ w[0];
-    if (cnt > 1) t ^= seg_map(w[1], kMapG + 7, lds);
-#pragma unroll
-    for (uint32_t c = 2; c < kMidChunk; c++)
-      if (c < cnt) t ^= nibble_map_set<kMidMaps>(w[c], lds, kLdsMidOff, c - 2);
-    return t;
+    for (uint32_t c = 0; c < kMidChunk; c++) a[c] = c < cnt ? w0 + 8 * c : 0u;
   }
 
   // Phase A: descriptor, plan, window and register loads (nothing the line pass writes).
@@ -372,29 +345,17 @@ struct Stitcher {
   // lane's payload has a run to join.
   __device__ __forceinline__ uint32_t mid_join(uint32_t acc, bool on, const Plan& y, Vals& v) const {
     const bool lng = on && y.nmid > kLongMid;
-    if (on && !lng && y.nmid) {
-      if constexpr (MID) {
-        acc = mid_level(acc, y.nmid < kMidChunk ? y.nmid : kMidChunk, v.mid);
-        for (uint32_t i = kMidChunk; i < y.nmid; i += kMidChunk) {
-          const uint32_t cnt = y.nmid - i < kMidChunk ? y.nmid - i : kMidChunk;
-          uint32_t ma[kMidChunk], w[kMidChunk];
-          mid_addrs(y.mid_s + i, cnt, ma);
+    if (on && !lng && y.nmid) {  // acc = shift_8KiB(acc) ^ SB[s, 0], superblock by superblock
+      for (uint32_t i = 0; i < y.nmid; i += kMidChunk) {
+        if (i > 0) {
+          uint32_t ma[kMidChunk];
+          mid_addrs(y.mid_s + i, y.nmid - i < kMidChunk ? y.nmid - i : kMidChunk, ma);
 #pragma unroll
-          for (uint32_t c = 0; c < kMidChunk; c++) w[c] = word(ma[c]);
-          acc = mid_level(acc, cnt, w);
+          for (uint32_t c = 0; c < kMidChunk; c++) v.mid[c] = word(ma[c]);
         }
-      } else {  // acc = shift_8KiB(acc) ^ SB[s, 0], superblock by superblock
-        for (uint32_t i = 0; i < y.nmid; i += kMidChunk) {
-          if (i > 0) {
-            uint32_t ma[kMidChunk];
-            mid_addrs(y.mid_s + i, y.nmid - i < kMidChunk ? y.nmid - i : kMidChunk, ma);
 #pragma unroll
-            for (uint32_t c = 0; c < kMidChunk; c++) v.mid[c] = word(ma[c]);
-          }
-#pragma unroll
-          for (uint32_t c = 0; c < kMidChunk; c++)
-            if (i + c < y.nmid) acc = seg_map(acc, kMapG + 7, lds) ^ v.mid[c];
-        }
+        for (uint32_t c = 0; c < kMidChunk; c++)
+          if (i + c < y.nmid) acc = seg_map(acc, kMapG + 7, lds) ^ v.mid[c];
       }
     }
     // the lanes running this (the payload loop leaves a wave's last lanes behind at the end of a block's range): they
@@ -451,8 +412,10 @@ struct Stitcher {
         g.out[p] = t;
       } else if (y.fast) {
         live = true;
-        mask_line<4>(v.h, (int32_t)y.hlo * 8, (int32_t)y.hhi * 8);
-        mask_line<4>(v.t, (int32_t)y.tlo * 8, (int32_t)y.thi * 8);
+        // (byte masks from the image's chunk tables: 2 LDS reads and 4 ands per chunk where mask_line's per-dword
+        // clamps and 64-bit shifts took about 200 VALU instructions per payload)
+        mask_chunks<4>(v.h, (int32_t)y.hlo, (int32_t)y.hhi, lds, kLdsStitchMaskOff);
+        mask_chunks<4>(v.t, (int32_t)y.tlo, (int32_t)y.thi, lds, kLdsStitchMaskOff);
         uint32_t wh;
         absorb_two_windows(v.h, v.t, k, lds, wh, wt);
         // head: V(first line start) = shift_{-lead}(s0) ^ shift_{-64}(wh), or
@@ -530,7 +493,7 @@ __device__ __forceinline__ void publish_extent(ExtentHint* host, uint64_t lo, ui
 // the same count for every block; the first payload's loads are in flight while the LDS image is staged.
 //   PIPE (microbench A/B, product = 0): 1 = the next payload's loads are issued before the
 //   current one is folded; 2 = a lane's first two payloads' descriptors and plan loads issued together.
-template <bool UPD, int BLK = kStitchBlock, int PROBE = 0, int PIPE = 0, bool MID = false, bool VER = false>
+template <bool UPD, int BLK = kStitchBlock, int PROBE = 0, int PIPE = 0, bool VER = false>
 __global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchGeo g0, const uint4* __restrict__ img_slice,
                                                                  const uint4* __restrict__ img_stitch) {
   __shared__ __attribute__((aligned(16))) uint4 lds4[kLdsStitchImageBytes / 16];
@@ -553,7 +516,7 @@ __global__ __launch_bounds__(BLK) void crc32_arena_stitch_kernel(StitchGeo g0, c
     if (blockIdx.x == 0 && threadIdx.x == 0 && g.record)  // the next calls' record (crc32_kernels.h)
       publish_extent(g.record, lo, hi, sum, bad, g.record_seq);
   }
-  const Stitcher<UPD, PROBE, MID, VER> st{g, reinterpret_cast<const uint32_t*>(lds4), lane_ctx()};
+  const Stitcher<UPD, PROBE, VER> st{g, reinterpret_cast<const uint32_t*>(lds4), lane_ctx()};
   const size_t per = (g.n + gridDim.x - 1) / gridDim.x;
   const size_t p_end = std::min(g.n, (size_t)(blockIdx.x + 1) * per);
   Plan y{};
@@ -1018,7 +981,7 @@ ArenaGeom launch_geom(const ArenaLaunch& a) {
   return a.choice.ws ? arena_geom_of(0, a.choice.blocks) : arena_geom(a);
 }
 
-template <int PROBE, int PIPE = 0, int BLK = kStitchBlock, bool MID = false>
+template <int PROBE, int PIPE = 0, int BLK = kStitchBlock>
 hipError_t launch_stitch_p(const ArenaLaunch& a, hipStream_t stream) {
   const StitchGeo s = stitch_geo(a, launch_geom(a));
   const size_t blocks = stitch_blocks(a, BLK);
@@ -1026,16 +989,16 @@ hipError_t launch_stitch_p(const ArenaLaunch& a, hipStream_t stream) {
   const uint4* img_stitch = static_cast<const uint4*>(a.img_stitch);
   if (a.ok && !a.update) {  // LengthHeaderCodec verify: the trailer compare in the stitch
     note_kernel("crc32_arena_stitch_kernel<verify>");
-    hipLaunchKernelGGL((crc32_arena_stitch_kernel<false, BLK, PROBE, PIPE, MID, true>), dim3((unsigned)blocks),
+    hipLaunchKernelGGL((crc32_arena_stitch_kernel<false, BLK, PROBE, PIPE, true>), dim3((unsigned)blocks),
                        dim3(BLK), 0, stream, s, img_slice, img_stitch);
     return hipGetLastError();
   }
   note_kernel("crc32_arena_stitch_kernel");
   if (a.update)
-    hipLaunchKernelGGL((crc32_arena_stitch_kernel<true, BLK, PROBE, PIPE, MID>), dim3((unsigned)blocks), dim3(BLK), 0,
+    hipLaunchKernelGGL((crc32_arena_stitch_kernel<true, BLK, PROBE, PIPE>), dim3((unsigned)blocks), dim3(BLK), 0,
                        stream, s, img_slice, img_stitch);
   else
-    hipLaunchKernelGGL((crc32_arena_stitch_kernel<false, BLK, PROBE, PIPE, MID>), dim3((unsigned)blocks), dim3(BLK), 0,
+    hipLaunchKernelGGL((crc32_arena_stitch_kernel<false, BLK, PROBE, PIPE>), dim3((unsigned)blocks), dim3(BLK), 0,
                        stream, s, img_slice, img_stitch);
   return hipGetLastError();
 }
@@ -1075,19 +1038,17 @@ hipError_t launch_arena(const ArenaLaunch& a, hipStream_t stream) {
   // 0.2139-0.2142 ms vs 0.2144-0.2151 without, same box, three alternating pairs
   // (profiles/r02/stitch_pipe_bench_ab/). 768-lane blocks with one payload in flight (3 waves per SIMD under a
   // 168-VGPR cap, no spill) measured 21.3 us against 20.4 for this 512-lane form (profiles/r03/stitch_ab/):
-  // occupancy is not what bounds it. A/B builds: ANNETY_CRC_STITCH_PIPE=0 (one payload at a time),
-  // ANNETY_CRC_STITCH_MID=1 (the one-level superblock join, which fits the VGPRs only without PIPE; measured
-  // no faster).
+  // occupancy is not what bounds it. A/B builds: ANNETY_CRC_STITCH_PIPE=0 (one payload at a time). (A one-level join
+  // of up to 7 whole superblocks from a table of shift_{c 8KiB} maps measured no faster than the chain, and was
+  // dropped in round 6 for the window masks' tables.)
 #ifdef ANNETY_CRC_AB
   static const bool pipe = ANNETY_AB_KNOB("ANNETY_CRC_STITCH_PIPE", 1) != 0;
-  static const bool mid = ANNETY_AB_KNOB("ANNETY_CRC_STITCH_MID", 0) == 1;
   static const int probe = ANNETY_AB_KNOB("ANNETY_CRC_STITCH_PROBE", 0);  // Stitcher PROBE (wrong digests)
   if (probe == 1) return launch_stitch_p<1, 1>(a, stream);
   if (probe == 2) return launch_stitch_p<2, 1>(a, stream);
   if (probe == 3) return launch_stitch_p<3, 1>(a, stream);
   if (probe == 4) return launch_stitch_p<4, 1>(a, stream);
   if (probe == 5) return launch_stitch_p<5, 1>(a, stream);
-  if (mid) return launch_stitch_p<0, 0, kStitchBlock, true>(a, stream);
   if (!pipe) return launch_stitch_p<0>(a, stream);
 #endif
   return launch_stitch_p<0, 1>(a, stream);

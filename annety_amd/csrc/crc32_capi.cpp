@@ -99,6 +99,16 @@ void put_set(uint32_t* dst, const uint32_t* maps, uint32_t T) {
       for (uint32_t v = 0; v < 16; v++) dst[(kk * T + i) * 16 + v] = maps[i * 128 + kk * 16 + v];
 }
 
+// Byte masks of a 16-byte chunk (crc32_device.h mask_chunks): KEEP_FROM[a] = bytes [a, 16) for a = 0..16, then
+// KEEP_TO[b] = bytes [0, b) for b = 0..16, 4 words each (544 bytes; dst zeroed).
+void chunk_masks(uint32_t* mk) {
+  for (uint32_t a = 0; a <= 16; a++)
+    for (uint32_t byte = 0; byte < 16; byte++) {
+      if (byte >= a) mk[a * 4 + byte / 4] |= 0xFFu << (8 * (byte % 4));
+      if (byte < a) mk[(17 + a) * 4 + byte / 4] |= 0xFFu << (8 * (byte % 4));
+    }
+}
+
 Gf2Mat gf2_inverse(const Gf2Mat& m) {
   // Gauss-Jordan over GF(2) on rows of the 32x32 matrix (row r = bit r of every column)
   uint64_t rows[32];
@@ -207,9 +217,7 @@ const HostImages& host_images() {
       put_set(m + (kLdsStitchUnshiftOff - kLdsMapOff) / 4, img.unshift.data(), 16);                  // U_lo
       put_set(m + (kLdsStitchUnshiftOff + 8192 - kLdsMapOff) / 4, img.unshift.data() + 16 * 128, 8);  // U_hi
       nibble_tables(shift_matrix(32), m + (kLdsQuarterOff - kLdsMapOff) / 4);
-      std::vector<uint32_t> mid(kMidMaps * 128);  // P(c) = shift_{c*8KiB}, c = 2..7
-      for (uint32_t c = 2; c < 2 + kMidMaps; c++) nibble_tables(shift_matrix((uint64_t)8192 * c), mid.data() + (c - 2) * 128);
-      put_set(m + (kLdsMidOff - kLdsMapOff) / 4, mid.data(), kMidMaps);
+      chunk_masks(m + (kLdsStitchMaskOff - kLdsMapOff) / 4);
     }
     img.w8.assign(kW8ImgBytes / 4, 0);
     {
@@ -230,12 +238,7 @@ const HostImages& host_images() {
       std::memcpy(m + (kLdsW8UnshiftOff - kLdsCommonBytes) / 4, img.unshift.data(), img.unshift.size() * 4);
       for (uint32_t lead = 0; lead < 128; lead++)
         m[(kLdsW8InitOff - kLdsCommonBytes) / 4 + lead] = gf2_apply(shift_matrix(128 - lead), kInit);
-      uint32_t* mk = m + (kLdsW8MaskOff - kLdsCommonBytes) / 4;  // KEEP_FROM[a], then KEEP_TO[b]
-      for (uint32_t a = 0; a <= 16; a++)
-        for (uint32_t byte = 0; byte < 16; byte++) {
-          if (byte >= a) mk[a * 4 + byte / 4] |= 0xFFu << (8 * (byte % 4));
-          if (byte < a) mk[(17 + a) * 4 + byte / 4] |= 0xFFu << (8 * (byte % 4));
-        }
+      chunk_masks(m + (kLdsW8MaskOff - kLdsCommonBytes) / 4);
     }
   });
   return img;

@@ -261,11 +261,13 @@ __device__ __forceinline__ void gstore16_nt(uint64_t addr, uint4 v) {
   asm volatile("global_store_dwordx4 %0, %1, off nt" ::"v"(addr), "v"(x) : "memory");
 }
 
-// Keep bytes [lo, hi) of N 16-byte chunks (N = 4: a half line), zero the rest, from the w8 image's chunk masks
-// (crc32_math.h kLdsW8MaskOff): per chunk two ds_read_b128 and four ands, against mask_line's per-word shifts.
+// Keep bytes [lo, hi) of N 16-byte chunks (N = 4: a half line), zero the rest, from an image's chunk masks at LDS
+// byte offset `off` (crc32_math.h kLdsW8MaskOff, kLdsStitchMaskOff: KEEP_FROM[a] = bytes [a, 16), then KEEP_TO[b] =
+// bytes [0, b)): per chunk two ds_read_b128 and four ands, against mask_line's per-word shifts.
 template <int N>
-__device__ __forceinline__ void mask_chunks(uint4 (&v)[N], int32_t lo, int32_t hi, const uint32_t* lds) {
-  const uint4* t = reinterpret_cast<const uint4*>(lds + kLdsW8MaskOff / 4);
+__device__ __forceinline__ void mask_chunks(uint4 (&v)[N], int32_t lo, int32_t hi, const uint32_t* lds,
+                                            uint32_t off = kLdsW8MaskOff) {
+  const uint4* t = reinterpret_cast<const uint4*>(lds + off / 4);
 #pragma unroll
   for (int i = 0; i < N; i++) {
     const uint4 a = t[min(max(lo - 16 * i, 0), 16)], b = t[17 + min(max(hi - 16 * i, 0), 16)];

@@ -131,16 +131,14 @@ constexpr uint32_t kLdsArenaNtImageBytes = kLdsArenaImageBytes + kLdsByteMapByte
 //   [kLdsStitchUnshiftOff, +8 KiB)  set U_lo[m] = shift_{-m}, (k, m, v) at (k*16 + m)*64 + v*4
 //   [+8 KiB, +12 KiB)                set U_hi[h] = shift_{-16h}, (k, h, v) at (k*8 + h)*64 + v*4
 //   [kLdsQuarterOff, +512)  shift_32 (joins the two 32-byte chains of a half-line window)
-//   [kLdsMidOff, +3 KiB)    set P(m) = shift_{m*8KiB}, m = 2..7, (k, m-2, v) at (k*6 + m-2)*64 + v*4: the whole
-//                           superblocks between a payload's partial ones, combined in one level
+//   [kLdsStitchMaskOff, +544 B)  byte masks of a 16-byte chunk (as kLdsW8MaskOff): the windows' kept bytes
 constexpr uint32_t kLdsMapOff = kLdsCommonBytes;
 constexpr uint32_t kLdsMapBytes = 32 * 512;
 constexpr uint32_t kMapF = 0, kMapG = 8, kMapUL = 16, kMapUB = 24;  // map index of F(1), G(1), UL(0), UB(0)
 constexpr uint32_t kLdsStitchUnshiftOff = kLdsMapOff + kLdsMapBytes;
 constexpr uint32_t kLdsQuarterOff = kLdsStitchUnshiftOff + kLdsUnshiftBytes;
-constexpr uint32_t kLdsMidOff = kLdsQuarterOff + 512;
-constexpr uint32_t kMidMaps = 6;  // P(2..7); P(1) = G(8) of the segment set, P(0) = identity
-constexpr uint32_t kLdsStitchImageBytes = kLdsMidOff + kMidMaps * 512;  // 163840: all of the CU's LDS
+constexpr uint32_t kLdsStitchMaskOff = kLdsQuarterOff + 512;
+constexpr uint32_t kLdsStitchImageBytes = kLdsStitchMaskOff + 544;  // 161312
 // Length-sorted path (crc32_kernels.hip var_class_w8): common part, then the
 // device image "w8" (kW8ImgBytes):
 //   [kLdsW8JoinOff, +4 KiB)     lane-position join, unreplicated: (k, v, j) at (k*16 + v)*32 + j*4 =
