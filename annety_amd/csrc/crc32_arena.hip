@@ -20,8 +20,9 @@
 //             E), appended to V(last line start).
 //     The whole lines between take at most four steps acc = M1(acc) ^ M2(S[a] ^ S[b]) (the head block,
 //     the partial superblocks' block runs, the tail block: M1 = shift by the unit, M2 = the inverse
-//     shift that cuts a suffix difference down to the unit); the whole superblocks between join in one
-//     level, acc = shift_{n*8KiB}(acc) ^ xor_q shift_{(n-1-q)*8KiB}(SB[q, 0]), n independent lookups.
+//     shift that cuts a suffix difference down to the unit); the whole superblocks between are a chain
+//     acc = shift_8KiB(acc) ^ SB[q, 0], shared by the lanes running the stitch once a run is longer than
+//     kLongMid superblocks (mid_join).
 //     A config-3 payload (6.5 KiB on average) costs 64 + 64 bytes of window folds and about six map
 //     steps of 8 nibble-table lookups, with every load issued before the first fold.
 //     s = 0xFFFFFFFF (crc32_long) or the caller's register (crc32_update, include/Crc32c.h:71-82).
