@@ -219,7 +219,7 @@ const HostImages& host_images() {
       nibble_tables(shift_matrix(32), m + (kLdsQuarterOff - kLdsMapOff) / 4);
       chunk_masks(m + (kLdsStitchMaskOff - kLdsMapOff) / 4);
     }
-    img.w8.assign(kW8ImgBytes / 4, 0);
+    img.w8.assign(kW8ImgAllBytes / 4, 0);
     {
       uint32_t* m = img.w8.data();
       for (uint32_t jj = 0; jj < 8; jj++) {  // (k, v, j) at (k*16 + v)*8 + j words
@@ -228,10 +228,12 @@ const HostImages& host_images() {
         for (int kk = 0; kk < 8; kk++)
           for (int v = 0; v < 16; v++) m[(kk * 16 + v) * 8 + jj] = nt[kk * 16 + v];
       }
-      const uint64_t shifts[2] = {64, 7 * kChunkBytes};  // byte tables: half-line join, round advance
-      for (int m_i = 0; m_i < 2; m_i++) {
+      // byte tables: half-line join, round advance (8-lane groups), round advance of 4-lane groups (the encode)
+      const uint64_t shifts[3] = {64, 7 * kChunkBytes, 3 * kChunkBytes};
+      const uint32_t offs[3] = {kLdsW8HalfOff, kLdsW8RoundOff, kLdsW8Round4Off};
+      for (int m_i = 0; m_i < 3; m_i++) {
         const Gf2Mat sm = shift_matrix(shifts[m_i]);
-        uint32_t* bm = m + (kLdsW8HalfOff - kLdsCommonBytes + m_i * 4096) / 4;
+        uint32_t* bm = m + (offs[m_i] - kLdsCommonBytes) / 4;
         for (uint32_t kk = 0; kk < 4; kk++)
           for (uint32_t e = 0; e < 256; e++) bm[kk * 256 + e] = gf2_apply(sm, e << (8 * kk));
       }
@@ -1437,6 +1439,8 @@ static int encode_batch(const FrameRules& r, const void* d_src, const uint64_t* 
   lg.seg_dst = reinterpret_cast<uint64_t*>(scratch + 8 * kEncLongCap + 16 * kEncLongSegCap);
   // one pass: each payload read once, its frame (header, copy, CRC trailer) written once (crc32_frames.hip); the
   // long frames it hands over: their digests on the sorted kernel (segments), then their copy, headers and trailers
+  // (lanes per frame: 4 when most frames fit one 4-line round - 408-byte chat frames: 0.594 -> 0.427 ms for 2M - else
+  // 8 - frames of 16 B - 1 KiB: 0.646 ms against 0.83 with 4; the two instances choose on the device, crc32_frames.hip)
   hipError_t e = launch_lhc_encode_fused(d_src, d_src_off, d_len, n, r.T, r.enc_min, r.enc_max, d_dst, d_frame_off,
                                          c->d_zero, c->d_slice, c->d_w8, lg, grid_cus(*c), s);
   if (e == hipSuccess) {

@@ -157,6 +157,12 @@ constexpr uint32_t kLdsW8InitOff = kLdsW8UnshiftOff + kLdsUnshiftBytes;
 constexpr uint32_t kLdsW8MaskOff = kLdsW8InitOff + 512;
 constexpr uint32_t kLdsW8ImageBytes = kLdsW8MaskOff + 544;            // 157216
 constexpr uint32_t kW8ImgBytes = kLdsW8ImageBytes - kLdsCommonBytes;  // 25632
+// The frame encode with lane groups of 4 (crc32_frames.hip lhc_encode_fused_kernel<P, 4>) advances its columns by 4
+// lines per round: byte tables of shift_{3*128} right after the w8 image (the device buffer holds them behind it;
+// the sorted kernel stages only kLdsW8ImageBytes)
+constexpr uint32_t kLdsW8Round4Off = kLdsW8ImageBytes;
+constexpr uint32_t kLdsEnc4ImageBytes = kLdsW8Round4Off + 4096;  // 161312
+constexpr uint32_t kW8ImgAllBytes = kLdsEnc4ImageBytes - kLdsCommonBytes;
 // after the image: each wave's ring of 4 claimed sets' descriptors (8 x 16 B a set), their set indices, and the
 // block's set counters (front, back: 2 x 32 bits of one 64-bit word)
 // The sorted kernel's block: 768 threads (12 waves: 3 per SIMD at <= 168 VGPRs) share the one LDS image.

@@ -1,5 +1,5 @@
 # Same-box A/B of two full library builds (ANNETY_CRC_LIB): bench lines alternating twice, then a rocprofv3 kernel
-# trace of each line with each library. Usage: r06_ab_libs.sh <out> <libA> <libB> <lines...> (lines: c3a fmv fcv c3s)
+# trace of each line with each library. Usage: r06_ab_libs.sh <out> <libA> <libB> <lines...> (c3a c3s fmv fcv fme fce)
 set -e
 O=$GRAFT_REPO_ROOT/gpurun_out/$1; mkdir -p $O; cd $GRAFT_REPO_ROOT
 export TMPDIR=/tmp
@@ -10,6 +10,8 @@ args() {
     c3s) echo "--config 3 --var-path sorted";;
     fmv) echo "--config frames --frames mixed --op verify";;
     fcv) echo "--config frames --frames chat --op verify";;
+    fme) echo "--config frames --frames mixed --op encode";;
+    fce) echo "--config frames --frames chat --op encode";;
   esac
 }
 for rep in 1 2; do

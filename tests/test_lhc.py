@@ -230,6 +230,30 @@ def test_gpu_encode_fused_every_alignment(gpu):
         assert frames == want, T
 
 
+@pytest.mark.gpu
+def test_gpu_encode_four_lane_groups(gpu):
+    """Batches of mostly short frames run the encoder with 4 lanes per frame (crc32_frames.hip lhc_encode_fused_kernel
+    picks it when >= 3/4 of 512 sampled frames fit one 4-line round): short frames at every source alignment, frames
+    of several 4-line rounds among them (lengths around whole lines and rounds), empty ones, and frames of more than
+    256 KiB that the 4-lane groups hand to the long path; every header width, every frame against the oracle."""
+    import torch
+
+    rng = np.random.default_rng(4)
+    short = rng.integers(0, 497, 3000)
+    multi = np.array([128 * k + d for k in range(3, 28) for d in (-3, 0, 5)])  # 2 to 7 rounds of 4 lines
+    lens = rng.permutation(np.concatenate([short, multi, [300000, 262145, 400000]])).astype(np.uint32)
+    starts = rng.integers(0, 128, lens.size).astype(np.uint64)
+    offs = np.concatenate([[0], np.cumsum((lens.astype(np.uint64) + 127) // 128 * 128 + 128)[:-1]]) + starts
+    arena = oracle.lcg_bytes(int(offs[-1] + lens[-1]) + 256, 321)
+    d_src = torch.from_numpy(arena.copy()).to(gpu)
+    for T, maxp in ((1, 100), (2, 30000), (4, 1 << 26), (8, 1 << 26)):
+        codec = LengthHeaderCodec(T, True, maxp)
+        r = codec.encode_batch(d_src, offs.astype(np.uint64), lens)
+        frames = r.frames.cpu().numpy().tobytes()
+        want = b"".join(oracle.lhc_encode(arena[int(o): int(o) + int(L)], T, maxp)[1] for o, L in zip(offs, lens))
+        assert frames == want, T
+
+
 # ---------------- the reference codec itself, linked against the drop-in ----------------
 @pytest.mark.skipif(not os.path.isdir("/root/reference/src"), reason="reference tree not present")
 def test_reference_codec_runs_on_dropin(golden, tmp_path):
