@@ -39,17 +39,18 @@ __global__ __launch_bounds__(256) void lhc_compare_kernel(const uint8_t* __restr
 // ---------------------------------------------------------------------------------------------
 // Fused LengthHeaderCodec encode (round 5; LengthHeaderCodec::encode :146-201 over a batch): each payload is read
 // once, with the coalesced 1 KiB loads of the sorted path (crc32_kernels.hip var_class_w8), and each frame written
-// once, with coalesced 16-byte stores at the frame's byte shift. One lane group of 8 per frame (frames i = group,
-// group + groups, ...), the payload [A, E) cut into VIRTUAL lines of 128 bytes from a0 = A rounded down to 16:
-// every load is an aligned 16-byte chunk (the chunks past the payload's last one re-read it, so no load leaves the
-// payload's chunks), and only the lead = A - a0 < 16 bytes before the payload and the bytes after E need masks.
-// Rounds as var_class_w8 (a head round of the first h lines, start-aligned, then rounds of 8 lines).
+// once, with coalesced 16-byte stores at the frame's byte shift. One lane group of G = 8 (or 4, round 6: chosen per
+// call from sampled lengths, lhc_encode_fused_kernel) per frame (frames i = group, group + groups, ...), the payload
+// [A, E) cut into VIRTUAL lines of 128 bytes from a0 = A rounded down to 16: every load is an aligned 16-byte chunk
+// (the chunks past the payload's last one re-read it, so no load leaves the payload's chunks), and only the lead =
+// A - a0 < 16 bytes before the payload and the bytes after E need masks. Rounds as var_class_w8 (a head round of
+// the first h lines, start-aligned, then rounds of G lines).
 //   * the copy, before the transpose: a chunk wholly inside the payload is stored as it is at its source address +
 //     (destination - A), unaligned; the <= 2 partial chunks of a frame (loaded once more, by lanes 0 and 1 of the
 //     group, with the round) store their payload bytes as 8/4/2/1-byte pieces;
 //   * the CRC: var_class_w8's round (transpose, fold, masked head and last rounds), the init as the register
 //     shift_{128-lead}(init) of line 0, the join and the inverse shift of the last line's overhang;
-//   * lane 7 of the group stores the T header bytes and the 4 trailer bytes (big-endian) when the frame ends.
+//   * the group's last lane stores the T header bytes and the 4 trailer bytes (big-endian) when the frame ends.
 // Frames the reference would not write (empty, or length outside [enc_min, enc_max]) get no bytes (the host plan
 // gave them none); they read the library's zero line. Algorithmic traffic: the payload read once, the frame
 // written once.
